@@ -1,0 +1,274 @@
+// curve.h -- G1 / G2 Jacobian group law and the G2 line steps of the flipped
+// Miller loop, one lane per point.
+//
+// Replaces src/groups/mod.rs:45-369 (generic G<P>), 371-472 (G1/G2 params),
+// 515-564 (twist constants) and 693-776 (line steps).  The projective formulas
+// are the reference's own -- they decide the Jacobian representation and the
+// line coefficients, both of which are observable (G1*Fr output, pre-FE Miller
+// values) -- so every coordinate is the same residue the reference computes.
+#pragma once
+#include "tower.h"
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BN_ANY(p) (__any((int)(p)) != 0)
+#else
+#define BN_ANY(p) (p)
+#endif
+
+namespace bn {
+
+// ---------------------------------------------------------------- base-field dispatch
+template <int A, int B>
+BN_INLINE auto F_add(const Fq<A>& a, const Fq<B>& b) { return fq_add(a, b); }
+template <int A, int B>
+BN_INLINE auto F_add(const Fq2<A>& a, const Fq2<B>& b) { return fq2_add(a, b); }
+template <int A, int B>
+BN_INLINE auto F_sub(const Fq<A>& a, const Fq<B>& b) { return fq_sub(a, b); }
+template <int A, int B>
+BN_INLINE auto F_sub(const Fq2<A>& a, const Fq2<B>& b) { return fq2_sub(a, b); }
+template <int A, int B>
+BN_INLINE auto F_mul(const Fq<A>& a, const Fq<B>& b) { return fq_mul(a, b); }
+template <int A, int B>
+BN_INLINE auto F_mul(const Fq2<A>& a, const Fq2<B>& b) { return fq2_mul(a, b); }
+template <int A>
+BN_INLINE auto F_sqr(const Fq<A>& a) { return fq_sqr(a); }
+template <int A>
+BN_INLINE auto F_sqr(const Fq2<A>& a) { return fq2_sqr(a); }
+template <int A>
+BN_INLINE auto F_neg(const Fq<A>& a) { return fq_neg(a); }
+template <int A>
+BN_INLINE auto F_neg(const Fq2<A>& a) { return fq2_neg(a); }
+template <int A>
+BN_INLINE auto F_fold(const Fq<A>& a) { return fq_fold(a); }
+template <int A>
+BN_INLINE auto F_fold(const Fq2<A>& a) { return fq2_fold(a); }
+template <int A>
+BN_INLINE bool F_is_zero(const Fq<A>& a) { return fq_is_zero(a); }
+template <int A>
+BN_INLINE bool F_is_zero(const Fq2<A>& a) { return fq2_is_zero(a); }
+template <int A>
+BN_INLINE auto F_inv(const Fq<A>& a) { return fq_inv(a); }
+template <int A>
+BN_INLINE auto F_inv(const Fq2<A>& a) { return fq2_inv(a); }
+template <int B2, int B>
+BN_INLINE Fq<B2> F_widen(const Fq<B>& a) { return widen<B2>(a); }
+template <int B2, int B>
+BN_INLINE Fq2<B2> F_widen(const Fq2<B>& a) { return widen<B2>(a); }
+template <int B>
+BN_INLINE Fq<B> F_select(bool c, const Fq<B>& a, const Fq<B>& b) { return fq_select(c, a, b); }
+template <int B>
+BN_INLINE Fq2<B> F_select(bool c, const Fq2<B>& a, const Fq2<B>& b) { return fq2_select(c, a, b); }
+
+// keep a value at storage bound S: widen when it already fits, else fold to 2
+template <int S, template <int> class F, int B>
+BN_INLINE F<S> narrow(const F<B>& a) {
+    static_assert(S >= 2, "storage bound must admit a folded value");
+    if constexpr (B <= S) {
+        return F_widen<S>(a);
+    } else {
+        return F_widen<S>(F_fold(a));
+    }
+}
+
+// ---------------------------------------------------------------- Jacobian points
+// storage bound of point coordinates between group operations
+constexpr int kPt = 4;
+template <template <int> class F>
+struct Jac {
+    F<kPt> x, y, z;
+};
+using G1J = Jac<Fq>;
+using G2J = Jac<Fq2>;
+
+template <template <int> class F>
+BN_INLINE F<1> F_one();
+template <>
+BN_INLINE Fq<1> F_one<Fq>() { return fq_one(); }
+template <>
+BN_INLINE Fq2<1> F_one<Fq2>() { return fq2_one(); }
+template <template <int> class F>
+BN_INLINE F<1> F_zero();
+template <>
+BN_INLINE Fq<1> F_zero<Fq>() { return fq_zero(); }
+template <>
+BN_INLINE Fq2<1> F_zero<Fq2>() { return fq2_zero(); }
+
+// zero = (0, 1, 0), mod.rs:230-236
+template <template <int> class F>
+BN_INLINE Jac<F> jac_zero() {
+    return {F_widen<kPt>(F_zero<F>()), F_widen<kPt>(F_one<F>()), F_widen<kPt>(F_zero<F>())};
+}
+template <template <int> class F>
+BN_INLINE bool jac_is_zero(const Jac<F>& p) { return F_is_zero(p.z); }  // mod.rs:246-248
+
+// mod.rs:250-269
+template <template <int> class F>
+BN_INLINE Jac<F> jac_double(const Jac<F>& s) {
+    auto a = F_sqr(s.x);
+    auto b = F_sqr(s.y);
+    auto c = F_sqr(b);
+    auto d0 = F_sub(F_sub(F_sqr(F_add(s.x, b)), a), c);
+    auto d = F_add(d0, d0);
+    auto e = F_add(F_add(a, a), a);
+    auto f = F_sqr(e);
+    auto x3 = F_fold(F_sub(f, F_add(d, d)));
+    auto c2 = F_add(c, c);
+    auto c4 = F_add(c2, c2);
+    auto eight_c = F_add(c4, c4);
+    auto y1z1 = F_mul(s.y, s.z);
+    return {narrow<kPt>(x3), narrow<kPt>(F_sub(F_mul(e, F_sub(F_fold(d), x3)), eight_c)), narrow<kPt>(F_add(y1z1, y1z1))};
+}
+
+// mod.rs:294-334, including both zero short-cuts and the doubling branch
+template <template <int> class F>
+BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o) {
+    const bool s_zero = jac_is_zero(s);
+    const bool o_zero = jac_is_zero(o);
+    auto z1_squared = F_sqr(s.z);
+    auto z2_squared = F_sqr(o.z);
+    auto u1 = F_mul(s.x, z2_squared);
+    auto u2 = F_mul(o.x, z1_squared);
+    auto z1_cubed = F_mul(s.z, z1_squared);
+    auto z2_cubed = F_mul(o.z, z2_squared);
+    auto s1 = F_mul(s.y, z2_cubed);
+    auto s2 = F_mul(o.y, z1_cubed);
+    auto h = F_sub(u2, u1);
+    auto s2_minus_s1 = F_sub(s2, s1);
+    // u1 == u2 && s1 == s2  <=>  h == 0 && s2 - s1 == 0 (mod p)
+    const bool same = F_is_zero(h) && F_is_zero(s2_minus_s1);
+    auto i = F_sqr(F_add(h, h));
+    auto j = F_mul(h, i);
+    auto r = F_add(s2_minus_s1, s2_minus_s1);
+    auto v = F_mul(u1, i);
+    auto s1_j = F_mul(s1, j);
+    auto x3 = F_fold(F_sub(F_sub(F_sqr(r), j), F_add(v, v)));
+    auto y3 = F_sub(F_mul(r, F_sub(v, x3)), F_add(s1_j, s1_j));
+    auto z3 = F_mul(F_sub(F_sub(F_sqr(F_add(s.z, o.z)), z1_squared), z2_squared), h);
+    Jac<F> out = {narrow<kPt>(x3), narrow<kPt>(y3), narrow<kPt>(z3)};
+    if (BN_ANY(same && !s_zero && !o_zero)) {  // rare: wave-uniform guard
+        Jac<F> d = jac_double(s);
+        const bool take = same && !s_zero && !o_zero;
+        out = {F_select(take, d.x, out.x), F_select(take, d.y, out.y), F_select(take, d.z, out.z)};
+    }
+    out = {F_select(o_zero, s.x, out.x), F_select(o_zero, s.y, out.y), F_select(o_zero, s.z, out.z)};
+    out = {F_select(s_zero, o.x, out.x), F_select(s_zero, o.y, out.y), F_select(s_zero, o.z, out.z)};
+    return out;
+}
+
+// mod.rs:336-350
+template <template <int> class F>
+BN_INLINE Jac<F> jac_neg(const Jac<F>& a) {
+    const bool z = jac_is_zero(a);
+    return {a.x, F_select(z, a.y, F_neg(a.y)), a.z};
+}
+
+// MSB-first double-and-add over the 256 bits of the canonical scalar
+// (mod.rs:272-292).  The bit pattern differs per lane: both steps are computed
+// and selected, so every lane follows exactly the reference's chain and the
+// Jacobian output is bit-identical.
+template <template <int> class F>
+BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8]) {
+    Jac<F> res = jac_zero<F>();
+    bool found_one = false;
+    uint32_t w[8];  // scalar, shifted left one bit per step (no indexed private arrays)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = k[i];
+#pragma unroll 1
+    for (int bit = 255; bit >= 0; --bit) {
+        const bool b = w[7] >> 31;
+#pragma unroll
+        for (int i = 7; i > 0; --i) w[i] = (w[i] << 1) | (w[i - 1] >> 31);
+        w[0] <<= 1;
+        if (BN_ANY(found_one)) {
+            Jac<F> d = jac_double(res);
+            res = {F_select(found_one, d.x, res.x), F_select(found_one, d.y, res.y), F_select(found_one, d.z, res.z)};
+        }
+        if (BN_ANY(b)) {
+            Jac<F> a = jac_add(res, p);
+            res = {F_select(b, a.x, res.x), F_select(b, a.y, res.y), F_select(b, a.z, res.z)};
+            found_one = found_one || b;
+        }
+    }
+    return res;
+}
+
+// ---------------------------------------------------------------- curve constants
+BN_INLINE Fq2<1> xi_const() { return fq2_const(Limbs9{BN_XI_C0}, Limbs9{BN_XI_C1}); }
+BN_INLINE Fq2<1> g2_coeff_b() { return fq2_const(Limbs9{BN_G2B_C0}, Limbs9{BN_G2B_C1}); }  // mod.rs:452-467
+BN_INLINE Fq<1> two_inv() { return fq_from_limbs<1>(Limbs9{BN_TWO_INV}); }                  // mod.rs:521-528
+BN_INLINE Fq2<1> twist_mul_by_q_x() { return fq2_const(Limbs9{BN_TWIST_Q_X_C0}, Limbs9{BN_TWIST_Q_X_C1}); }
+BN_INLINE Fq2<1> twist_mul_by_q_y() { return fq2_const(Limbs9{BN_TWIST_Q_Y_C0}, Limbs9{BN_TWIST_Q_Y_C1}); }
+
+// ---------------------------------------------------------------- flipped Miller loop steps
+template <int B>
+struct G2Aff {
+    Fq2<B> x, y;
+};
+constexpr int kLine = 4;  // storage bound of line coefficients
+struct Ell {
+    Fq2<kLine> ell_0, ell_vw, ell_vv;
+};
+// homogeneous-projective R on the twist between steps
+struct G2Proj {
+    Fq2<kPt> x, y, z;
+};
+
+// mod.rs:754-776 -- the twist() * i product is xi * i (ring identity)
+BN_INLINE Ell doubling_step(G2Proj& s) {
+    auto a = fq2_scale(fq2_mul(s.x, s.y), two_inv());
+    auto b = fq2_sqr(s.y);
+    auto c = fq2_sqr(s.z);
+    auto d = fq2_add(fq2_add(c, c), c);
+    auto e = fq2_mul(g2_coeff_b(), d);
+    auto f = fq2_add(fq2_add(e, e), e);
+    auto g = fq2_scale(fq2_add(b, f), two_inv());
+    auto h = fq2_sub(fq2_sqr(fq2_add(s.y, s.z)), fq2_add(b, c));
+    auto i = fq2_sub(e, b);
+    auto j = fq2_sqr(s.x);
+    auto e_sq = fq2_sqr(e);
+    s.x = narrow<kPt>(fq2_mul(a, fq2_sub(b, f)));
+    s.y = narrow<kPt>(fq2_sub(fq2_sqr(g), fq2_add(fq2_add(e_sq, e_sq), e_sq)));
+    s.z = narrow<kPt>(fq2_mul(b, h));
+    return {narrow<kLine>(fq2_mul_xi(i)), narrow<kLine>(fq2_neg(h)), narrow<kLine>(fq2_add(fq2_add(j, j), j))};
+}
+// mod.rs:731-752
+template <int BB>
+BN_INLINE Ell mixed_addition_step(G2Proj& s, const G2Aff<BB>& base) {
+    auto d = fq2_sub(s.x, fq2_mul(s.z, base.x));
+    auto e = fq2_sub(s.y, fq2_mul(s.z, base.y));
+    auto f = fq2_sqr(d);
+    auto g = fq2_sqr(e);
+    auto h = fq2_mul(d, f);
+    auto i = fq2_mul(s.x, f);
+    auto j = fq2_sub(fq2_add(fq2_mul(s.z, g), h), fq2_add(i, i));
+    auto nx = fq2_mul(d, j);
+    auto ny = fq2_sub(fq2_mul(e, fq2_sub(i, j)), fq2_mul(h, s.y));
+    auto nz = fq2_mul(s.z, h);
+    s.x = narrow<kPt>(nx);
+    s.y = narrow<kPt>(ny);
+    s.z = narrow<kPt>(nz);
+    auto l0 = fq2_mul_xi(fq2_sub(fq2_mul(e, base.x), fq2_mul(d, base.y)));
+    return {narrow<kLine>(l0), narrow<kLine>(d), narrow<kLine>(fq2_neg(e))};
+}
+// mod.rs:694-699
+template <int B>
+BN_INLINE G2Aff<kPt> mul_by_q(const G2Aff<B>& q) {
+    return {narrow<kPt>(fq2_mul(twist_mul_by_q_x(), fq2_conj(q.x))), narrow<kPt>(fq2_mul(twist_mul_by_q_y(), fq2_conj(q.y)))};
+}
+
+// ATE_LOOP_COUNT_NAF, mod.rs:14 (3 == -1): 64 digits, 21 nonzero -> 87 lines.
+// Bit i of kNafNonzero / kNafMinus is digit i of the reference array.
+#define BN_NAF_DIGITS 64
+#define BN_NUM_COEFFS 87
+constexpr uint64_t naf_mask(int want) {
+    const uint8_t naf[64] = {1, 0, 1, 0, 0, 0, 3, 0, 3, 0, 0, 0, 3, 0, 1, 0, 3, 0, 0, 3, 0, 0, 0, 0, 0, 1, 0, 0, 3, 0, 1, 0,
+                             0, 3, 0, 0, 0, 0, 3, 0, 1, 0, 0, 0, 3, 0, 3, 0, 0, 1, 0, 0, 0, 3, 0, 0, 3, 0, 1, 0, 1, 0, 0, 0};
+    uint64_t m = 0;
+    for (int i = 0; i < 64; ++i)
+        if ((want == 0 && naf[i] != 0) || (want == 3 && naf[i] == 3)) m |= 1ull << i;
+    return m;
+}
+constexpr uint64_t kNafNonzero = naf_mask(0);
+constexpr uint64_t kNafMinus = naf_mask(3);
+
+}  // namespace bn

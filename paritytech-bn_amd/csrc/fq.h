@@ -1,0 +1,294 @@
+// fq.h -- BN254 base field Fq on CDNA4 (gfx950), one lane per element.
+//
+// Replaces src/arith.rs:281-316 + 473-545 and src/fields/fp.rs:7-164 of the
+// reference (U256 Montgomery arithmetic with 2 x u128 digits).
+//
+// Internal representation (chosen from measurements on MI355X):
+//   x is held as X = x * 2^261 mod p (Montgomery, R = 2^261) in NINE 29-bit
+//   digits, one per 32-bit VGPR.  29-bit digits let a column of the Montgomery
+//   product accumulate all 18 digit products in one 64-bit register with
+//   v_mad_u64_u32 and NO per-product carry instruction (on gfx950 a carry op
+//   costs as much as the multiply itself), and let additions/subtractions run
+//   digit-wise with full-rate VOP2 instructions.
+//
+//   Values are kept "weakly reduced": digits normalized (< 2^29) but the value
+//   may exceed p.  Fq<B> carries a compile-time bound: value <= B*p.  Every
+//   operation derives its output bound, and static_asserts keep every value
+//   below 2^261 and every column sum below 2^64 -- so no overflow is possible
+//   on any input.  Values become canonical (the reference's memory image) only
+//   at the boundary (fq_store_ref / fq_canonical).
+//
+// Bit-exactness: each function computes the same residue mod p as the
+// reference function it replaces, and the boundary emits the unique canonical
+// Montgomery image the reference stores.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BN_HD __host__ __device__
+#define BN_INLINE __host__ __device__ __forceinline__
+#else
+#define BN_HD
+#define BN_INLINE inline __attribute__((always_inline))
+#endif
+
+namespace bn {
+
+#include "constants.inc"
+
+constexpr uint32_t M29 = 0x1fffffffu;
+struct Limbs9 {
+    uint32_t v[9];
+};
+constexpr Limbs9 kP29 = {BN_P29};
+
+// value bound bookkeeping ------------------------------------------------
+// p / 2^261 < 0.005908 ; output of a Montgomery product of values <= A*p, <= B*p
+// is <= (1 + A*B*p/R) * p.
+constexpr int mul_bound(int A, int B) { return 1 + (int)(((long long)A * B * 5908 + 999999) / 1000000); }
+constexpr int kMaxBound = 160;  // 160 * p < 2^261
+
+template <int B>
+struct Fq {
+    static_assert(B >= 1 && B <= kMaxBound, "Fq value bound out of range");
+    uint32_t v[9];
+};
+
+// widen the static bound (free)
+template <int B2, int B>
+BN_INLINE Fq<B2> widen(const Fq<B>& a) {
+    static_assert(B <= B2, "widen: narrowing");
+    Fq<B2> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i];
+    return r;
+}
+
+template <int B = 1>
+BN_INLINE Fq<B> fq_from_limbs(const Limbs9& l) {
+    Fq<B> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = l.v[i];
+    return r;
+}
+BN_INLINE Fq<1> fq_zero() { return fq_from_limbs<1>(Limbs9{{0, 0, 0, 0, 0, 0, 0, 0, 0}}); }
+BN_INLINE Fq<1> fq_one() { return fq_from_limbs<1>(Limbs9{BN_ONE}); }
+
+// carry-propagate digits 0..7 into 8 (full-rate VOP2: lshr, and, add)
+template <int B>
+BN_INLINE void fq_normalize(Fq<B>& r) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        r.v[i + 1] += r.v[i] >> 29;
+        r.v[i] &= M29;
+    }
+}
+
+// a + b  (fq: arith.rs:281-287 computes the same residue)
+template <int A, int B>
+BN_INLINE Fq<A + B> fq_add(const Fq<A>& a, const Fq<B>& b) {
+    Fq<A + B> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + b.v[i];
+    fq_normalize(r);
+    return r;
+}
+template <int B>
+BN_INLINE Fq<2 * B> fq_dbl(const Fq<B>& a) { return fq_add(a, a); }
+
+// K*p with every digit but the top one raised into [2^29-1, 2^30): subtracting a
+// normalized value digit-wise from it never goes negative in digits 0..7; the top
+// digit is computed modulo 2^32 and is correct because the total is >= 0.
+constexpr Limbs9 kp_spread(int K) {
+    Limbs9 r = {{0, 0, 0, 0, 0, 0, 0, 0, 0}};
+    unsigned long long c = 0;
+    for (int i = 0; i < 9; ++i) {
+        unsigned long long t = (unsigned long long)K * kP29.v[i] + c;
+        r.v[i] = (uint32_t)(t & M29);
+        c = t >> 29;
+    }
+    r.v[0] += 1u << 29;
+    for (int i = 1; i < 8; ++i) r.v[i] += (1u << 29) - 1;
+    r.v[8] -= 1;
+    return r;
+}
+
+// a - b + B*p  (arith.rs:290-296 computes the same residue)
+template <int A, int B>
+BN_INLINE Fq<A + B> fq_sub(const Fq<A>& a, const Fq<B>& b) {
+    constexpr Limbs9 Q = kp_spread(B);
+    Fq<A + B> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = (a.v[i] + Q.v[i]) - b.v[i];
+    fq_normalize(r);
+    return r;
+}
+// B*p - a  (arith.rs:309-316: -0 stays 0, and B*p == 0 mod p)
+template <int B>
+BN_INLINE Fq<B> fq_neg(const Fq<B>& a) {
+    constexpr Limbs9 Q = kp_spread(B);
+    Fq<B> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = Q.v[i] - a.v[i];
+    fq_normalize(r);
+    return r;
+}
+
+// a * b * 2^-261 mod p: Montgomery product by finely integrated product
+// scanning.  Column k accumulates every a_i*b_j and m_i*p_j with i+j == k in a
+// 64-bit accumulator (18 products of < 2^58 each plus the carry-in stay below
+// 2^63), derives m_k = acc * (-p^-1) mod 2^29 for k < 9 so the low digit
+// cancels, then shifts by 29.  hipcc emits one v_mad_u64_u32 per product.
+template <int A, int B>
+BN_INLINE Fq<mul_bound(A, B)> fq_mul(const Fq<A>& a, const Fq<B>& b) {
+    static_assert((long long)A * B <= 160 * 160, "product bound");
+    uint32_t m[9];
+    Fq<mul_bound(A, B)> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        const int lo = k < 9 ? 0 : k - 8;
+        const int hi = k < 9 ? k : 8;
+#pragma unroll
+        for (int i = lo; i <= hi; ++i) {
+            acc += (uint64_t)a.v[i] * b.v[k - i];
+            if (i < k) acc += (uint64_t)m[i] * kP29.v[k - i];
+        }
+        if (k < 9) {
+            m[k] = ((uint32_t)acc * BN_PINV29) & M29;
+            acc += (uint64_t)m[k] * kP29.v[0];
+        } else {
+            r.v[k - 9] = (uint32_t)acc & M29;
+        }
+        acc >>= 29;
+    }
+    r.v[8] = (uint32_t)acc;
+    return r;
+}
+template <int B>
+BN_INLINE Fq<mul_bound(B, B)> fq_sqr(const Fq<B>& a) { return fq_mul(a, a); }
+
+// bring any value back to bound 2 (a Montgomery product with one)
+template <int B>
+BN_INLINE Fq<mul_bound(B, 1)> fq_reduce(const Fq<B>& a) { return fq_mul(a, fq_one()); }
+
+// x * c for a small constant c (digit-wise, then carry propagation)
+template <int C, int B>
+BN_INLINE Fq<C * B> fq_mul_small(const Fq<B>& a) {
+    static_assert(C >= 1 && C <= 8, "digit * C must fit 32 bits");
+    Fq<C * B> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] * C;
+    fq_normalize(r);
+    return r;
+}
+
+// Partial reduction to bound 2 without a multiplication: estimate
+// q <= floor(x/p) from the top digit (x8 * 2^232 / p, computed in f32 with a
+// constant rounded 2^-18 low so the estimate never overshoots), then x - q*p.
+// About a fifth of a Montgomery product; used where bounds would otherwise grow.
+template <int B>
+BN_INLINE Fq<2> fq_fold(const Fq<B>& x) {
+    const float c = 3.1531629e-07f;  // < 2^232/p * (1 - 2^-18)
+    const uint32_t q = (uint32_t)((float)x.v[8] * c);
+    Fq<2> r;
+    int64_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        int64_t t = (int64_t)x.v[i] - (int64_t)((uint64_t)q * kP29.v[i]) + carry;
+        r.v[i] = (uint32_t)t & M29;
+        carry = t >> 29;
+    }
+    r.v[8] = (uint32_t)((int64_t)x.v[8] - (int64_t)((uint64_t)q * kP29.v[8]) + carry);
+    return r;
+}
+
+// select (per lane)
+template <int B>
+BN_INLINE Fq<B> fq_select(bool c, const Fq<B>& a, const Fq<B>& b) {
+    Fq<B> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+    return r;
+}
+
+// ---------------------------------------------------------------- canonical forms
+// subtract p once if value >= p (input value < 2p)
+BN_INLINE Fq<1> fq_cond_sub_p(const Fq<2>& x) {
+    uint32_t d[9];
+    int32_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        int32_t t = (int32_t)x.v[i] - (int32_t)kP29.v[i] + borrow;
+        borrow = t >> 29;  // arithmetic: -1 on borrow
+        d[i] = (uint32_t)t & M29;
+    }
+    const bool ge = borrow == 0;  // x - p >= 0
+    Fq<1> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = ge ? d[i] : x.v[i];
+    return r;
+}
+// the unique representative in [0, p) of the same internal value (X mod p)
+template <int B>
+BN_INLINE Fq<1> fq_canonical(const Fq<B>& a) {
+    return fq_cond_sub_p(widen<2>(fq_reduce(a)));
+}
+template <int B>
+BN_INLINE bool fq_is_zero(const Fq<B>& a) {
+    Fq<1> c = fq_canonical(a);
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o |= c.v[i];
+    return o == 0;
+}
+template <int A, int B>
+BN_INLINE bool fq_eq(const Fq<A>& a, const Fq<B>& b) {
+    Fq<1> x = fq_canonical(a), y = fq_canonical(b);
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o |= x.v[i] ^ y.v[i];
+    return o == 0;
+}
+
+// ---------------------------------------------------------------- boundary
+// The reference memory image of an Fq: x*2^256 mod p, canonical, as eight
+// little-endian 32-bit words (== four u64 limbs == U256([u128;2])).
+BN_INLINE Fq<1> fq_digits_from_words(const uint32_t w[8]) {
+    Fq<1> r;  // plain repacking of a 256-bit integer into 29-bit digits
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const int bit = 29 * i, j = bit >> 5, s = bit & 31;
+        uint64_t lo = w[j];
+        uint64_t hi = (j + 1 < 8) ? w[j + 1] : 0;
+        r.v[i] = (uint32_t)(((hi << 32 | lo) >> s) & M29);
+    }
+    return r;
+}
+BN_INLINE void fq_words_from_digits(const Fq<1>& a, uint32_t w[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int bit = 32 * j, i = bit / 29, s = bit % 29;
+        uint64_t v = (uint64_t)a.v[i] >> s;
+        if (i + 1 < 9) v |= (uint64_t)a.v[i + 1] << (29 - s);
+        if (i + 2 < 9 && 58 - s < 32) v |= (uint64_t)a.v[i + 2] << (58 - s);
+        w[j] = (uint32_t)v;
+    }
+}
+// reference image (canonical x*2^256 mod p) -> internal
+BN_INLINE Fq<2> fq_load_ref(const uint32_t w[8]) {
+    return fq_mul(fq_digits_from_words(w), fq_from_limbs<1>(Limbs9{BN_TO_INTERNAL}));
+}
+// internal -> reference image, canonical
+template <int B>
+BN_INLINE void fq_store_ref(const Fq<B>& a, uint32_t w[8]) {
+    Fq<1> c = fq_cond_sub_p(widen<2>(fq_mul(a, fq_from_limbs<1>(Limbs9{BN_TO_REF}))));
+    fq_words_from_digits(c, w);
+}
+// canonical plain integer -> internal
+BN_INLINE Fq<2> fq_from_canonical_words(const uint32_t w[8]) {
+    return fq_mul(fq_digits_from_words(w), fq_from_limbs<1>(Limbs9{BN_FROM_CANON}));
+}
+
+}  // namespace bn

@@ -1,0 +1,381 @@
+// tower.h -- Fq2 / Fq6 / Fq12 tower of BN254 on CDNA4, one lane per element.
+//
+// Replaces src/fields/fq2.rs, fq6.rs, fq12.rs.  Each function returns the same
+// residue (mod p, per coefficient) as the reference function it cites; where
+// the formula differs it differs only by a ring identity (x * (p-1) is a
+// negation, x * xi with xi = 9+u is a digit-wise add chain, Fermat instead of
+// binary-Euclid inversion), never in the value.  Formulas that are NOT ring
+// identities -- Granger-Scott cyclotomic squaring, the sparse line product --
+// follow the reference's own expressions.
+//
+// Bounds: FqN<B> means every coefficient is an Fq<B> (value <= B*p).  Return
+// types are deduced, so the compiler proves every intermediate stays below
+// 2^261; fq*_fold() brings a value back to bound 2 where a formula would
+// otherwise overflow (the static_asserts in fq.h say where).
+#pragma once
+#include "fq.h"
+
+namespace bn {
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+template <int B>
+struct Fq2 {
+    Fq<B> c0, c1;
+};
+template <int B>
+struct Fq6 {
+    Fq2<B> c0, c1, c2;
+};
+template <int B>
+struct Fq12 {
+    Fq6<B> c0, c1;
+};
+
+// ================================================================ Fq2 = Fq[u]/(u^2+1)
+template <int A, int B>
+BN_INLINE Fq2<cmax(A, B)> mk2(const Fq<A>& x, const Fq<B>& y) {
+    return {widen<cmax(A, B)>(x), widen<cmax(A, B)>(y)};
+}
+template <int B2, int B>
+BN_INLINE Fq2<B2> widen(const Fq2<B>& a) { return {widen<B2>(a.c0), widen<B2>(a.c1)}; }
+
+BN_INLINE Fq2<1> fq2_zero() { return {fq_zero(), fq_zero()}; }
+BN_INLINE Fq2<1> fq2_one() { return {fq_one(), fq_zero()}; }
+template <int B>
+BN_INLINE Fq2<B> fq2_select(bool c, const Fq2<B>& a, const Fq2<B>& b) {
+    return {fq_select(c, a.c0, b.c0), fq_select(c, a.c1, b.c1)};
+}
+template <int A, int B>
+BN_INLINE Fq2<A + B> fq2_add(const Fq2<A>& a, const Fq2<B>& b) { return {fq_add(a.c0, b.c0), fq_add(a.c1, b.c1)}; }
+template <int A, int B>
+BN_INLINE Fq2<A + B> fq2_sub(const Fq2<A>& a, const Fq2<B>& b) { return {fq_sub(a.c0, b.c0), fq_sub(a.c1, b.c1)}; }
+template <int B>
+BN_INLINE Fq2<B> fq2_neg(const Fq2<B>& a) { return {fq_neg(a.c0), fq_neg(a.c1)}; }
+template <int B>
+BN_INLINE Fq2<2 * B> fq2_dbl(const Fq2<B>& a) { return fq2_add(a, a); }
+template <int B>
+BN_INLINE Fq2<2> fq2_fold(const Fq2<B>& a) { return {fq_fold(a.c0), fq_fold(a.c1)}; }
+template <int B>
+BN_INLINE bool fq2_is_zero(const Fq2<B>& a) { return fq_is_zero(a.c0) & fq_is_zero(a.c1); }
+// x unchanged when its bound is <= L, else folded to 2 (decided at compile time)
+template <int L, int B>
+BN_INLINE auto pre(const Fq<B>& a) {
+    if constexpr (B <= L) return a; else return fq_fold(a);
+}
+template <int L, int B>
+BN_INLINE auto pre(const Fq2<B>& a) {
+    if constexpr (B <= L) return a; else return fq2_fold(a);
+}
+template <int A, int B>
+BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) { return fq_eq(a.c0, b.c0) & fq_eq(a.c1, b.c1); }
+
+// fq2.rs:48-53
+template <int A, int B>
+BN_INLINE auto fq2_scale(const Fq2<A>& a, const Fq<B>& s) { return mk2(fq_mul(a.c0, s), fq_mul(a.c1, s)); }
+
+// fq2.rs:136-148 (Karatsuba; bb * (p-1) + aa == aa - bb)
+template <int A, int B>
+BN_INLINE auto fq2_mul(const Fq2<A>& a, const Fq2<B>& b) {
+    if constexpr (A > 40 || B > 40) return fq2_mul(pre<40>(a), pre<40>(b)); else {
+    auto aa = fq_mul(a.c0, b.c0);
+    auto bb = fq_mul(a.c1, b.c1);
+    auto t = fq_mul(fq_add(a.c0, a.c1), fq_add(b.c0, b.c1));
+    return mk2(fq_sub(aa, bb), fq_sub(fq_sub(t, aa), bb));
+    }
+}
+// fq2.rs:105-117: (c1*(p-1) + c0)(c0 + c1) - ab - ab*(p-1) == (c0 - c1)(c0 + c1); c1 = 2ab
+template <int A>
+BN_INLINE auto fq2_sqr(const Fq2<A>& a) {
+    if constexpr (A > 40) return fq2_sqr(fq2_fold(a)); else {
+    auto ab = fq_mul(a.c0, a.c1);
+    auto c0 = fq_mul(fq_sub(a.c0, a.c1), fq_add(a.c0, a.c1));
+    return mk2(c0, fq_dbl(ab));
+    }
+}
+// x * xi, xi = 9 + u (fq2.rs:19-34, 55-57): (9a0 - a1) + (a0 + 9a1) u.
+// Inputs above bound 15 are folded first so the result stays <= 150.
+template <int A>
+BN_INLINE auto fq2_mul_xi(const Fq2<A>& a) {
+    if constexpr (A > 15) {
+        return fq2_mul_xi(fq2_fold(a));
+    } else {
+        auto n0 = fq_add(fq_mul_small<8>(a.c0), a.c0);
+        auto n1 = fq_add(fq_mul_small<8>(a.c1), a.c1);
+        return mk2(fq_sub(n0, a.c1), fq_add(a.c0, n1));
+    }
+}
+// fq2.rs:59-68: odd powers conjugate (c1 * (p-1) == -c1)
+template <int B>
+BN_INLINE Fq2<B> fq2_conj(const Fq2<B>& a) { return {a.c0, fq_neg(a.c1)}; }
+
+// ---------------------------------------------------------------- inversion
+// Fermat: a^(p-2).  Inverses are unique, so this equals the reference's binary
+// extended Euclid (arith.rs:324-370 + fp.rs:108-117) bit for bit, without its
+// data-dependent control flow.  The exponent bit is uniform across the wave.
+BN_INLINE bool pm2_bit(int bit) {  // bits of p - 2
+    const uint64_t w = bit >= 192 ? 0x30644e72e131a029ull
+                     : bit >= 128 ? 0xb85045b68181585dull
+                     : bit >= 64  ? 0x97816a916871ca8dull
+                                  : 0x3c208c16d87cfd45ull;
+    return (w >> (bit & 63)) & 1u;
+}
+template <int B>
+BN_INLINE Fq<2> fq_inv(const Fq<B>& a) {
+    const Fq<2> x = widen<2>(fq_reduce(a));
+    Fq<2> r = x;  // bit 253 (top bit of p-2) is set
+#pragma unroll 1
+    for (int bit = 252; bit >= 0; --bit) {
+        r = fq_sqr(r);
+        if (pm2_bit(bit)) r = fq_mul(r, x);
+    }
+    return r;
+}
+// fq2.rs:119-130
+template <int B>
+BN_INLINE auto fq2_inv(const Fq2<B>& a_in) {
+    auto a = pre<40>(a_in);
+    auto t = fq_inv(fq_add(fq_sqr(a.c0), fq_sqr(a.c1)));  // c0^2 - (p-1) c1^2
+    return mk2(fq_mul(a.c0, t), fq_neg(fq_mul(a.c1, t)));
+}
+
+// ================================================================ Fq6 = Fq2[v]/(v^3 - xi)
+template <int A, int B, int C>
+BN_INLINE Fq6<cmax(A, cmax(B, C))> mk6(const Fq2<A>& x, const Fq2<B>& y, const Fq2<C>& z) {
+    constexpr int M = cmax(A, cmax(B, C));
+    return {widen<M>(x), widen<M>(y), widen<M>(z)};
+}
+template <int B2, int B>
+BN_INLINE Fq6<B2> widen(const Fq6<B>& a) { return {widen<B2>(a.c0), widen<B2>(a.c1), widen<B2>(a.c2)}; }
+BN_INLINE Fq6<1> fq6_zero() { return {fq2_zero(), fq2_zero(), fq2_zero()}; }
+BN_INLINE Fq6<1> fq6_one() { return {fq2_one(), fq2_zero(), fq2_zero()}; }
+template <int A, int B>
+BN_INLINE Fq6<A + B> fq6_add(const Fq6<A>& a, const Fq6<B>& b) {
+    return {fq2_add(a.c0, b.c0), fq2_add(a.c1, b.c1), fq2_add(a.c2, b.c2)};
+}
+template <int A, int B>
+BN_INLINE Fq6<A + B> fq6_sub(const Fq6<A>& a, const Fq6<B>& b) {
+    return {fq2_sub(a.c0, b.c0), fq2_sub(a.c1, b.c1), fq2_sub(a.c2, b.c2)};
+}
+template <int B>
+BN_INLINE Fq6<B> fq6_neg(const Fq6<B>& a) { return {fq2_neg(a.c0), fq2_neg(a.c1), fq2_neg(a.c2)}; }
+template <int B>
+BN_INLINE Fq6<2> fq6_fold(const Fq6<B>& a) { return {fq2_fold(a.c0), fq2_fold(a.c1), fq2_fold(a.c2)}; }
+template <int B>
+BN_INLINE bool fq6_is_zero(const Fq6<B>& a) { return fq2_is_zero(a.c0) & fq2_is_zero(a.c1) & fq2_is_zero(a.c2); }
+template <int L, int B>
+BN_INLINE auto pre(const Fq6<B>& a) {
+    if constexpr (B <= L) return a; else return fq6_fold(a);
+}
+// fq6.rs:109-115
+template <int B>
+BN_INLINE auto fq6_mul_by_nonresidue(const Fq6<B>& a) { return mk6(fq2_mul_xi(a.c2), a.c0, a.c1); }
+
+// fq6.rs:197-207
+template <int A, int B>
+BN_INLINE auto fq6_mul(const Fq6<A>& a, const Fq6<B>& b) {
+    if constexpr (A > 20 || B > 20) return fq6_mul(pre<20>(a), pre<20>(b)); else {
+    auto a_a = fq2_mul(a.c0, b.c0);
+    auto b_b = fq2_mul(a.c1, b.c1);
+    auto c_c = fq2_mul(a.c2, b.c2);
+    auto t0 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c1, a.c2), fq2_add(b.c1, b.c2)), b_b), c_c);
+    auto t1 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c0, a.c1), fq2_add(b.c0, b.c1)), a_a), b_b);
+    auto t2 = fq2_sub(fq2_mul(fq2_add(a.c0, a.c2), fq2_add(b.c0, b.c2)), a_a);
+    return mk6(fq2_add(fq2_mul_xi(t0), a_a), fq2_add(t1, fq2_mul_xi(c_c)), fq2_sub(fq2_add(t2, b_b), c_c));
+    }
+}
+// fq6.rs:163-177
+template <int A>
+BN_INLINE auto fq6_sqr(const Fq6<A>& a) {
+    if constexpr (A > 20) return fq6_sqr(fq6_fold(a)); else {
+    auto s0 = fq2_sqr(a.c0);
+    auto s1 = fq2_dbl(fq2_mul(a.c0, a.c1));
+    auto s2 = fq2_sqr(fq2_add(fq2_sub(a.c0, a.c1), a.c2));
+    auto s3 = fq2_dbl(fq2_mul(a.c1, a.c2));
+    auto s4 = fq2_sqr(a.c2);
+    return mk6(fq2_add(s0, fq2_mul_xi(s3)), fq2_add(s1, fq2_mul_xi(s4)),
+               fq2_sub(fq2_sub(fq2_add(fq2_add(s1, s2), s3), s0), s4));
+    }
+}
+// fq6.rs:179-191
+template <int B>
+BN_INLINE auto fq6_inv(const Fq6<B>& a_in) {
+    auto a = fq6_fold(a_in);
+    auto c0 = fq2_fold(fq2_sub(fq2_sqr(a.c0), fq2_mul(a.c1, fq2_mul_xi(a.c2))));
+    auto c1 = fq2_fold(fq2_sub(fq2_mul_xi(fq2_sqr(a.c2)), fq2_mul(a.c0, a.c1)));
+    auto c2 = fq2_fold(fq2_sub(fq2_sqr(a.c1), fq2_mul(a.c0, a.c2)));
+    auto t = fq2_inv(fq2_fold(fq2_add(fq2_mul_xi(fq2_add(fq2_mul(a.c2, c1), fq2_mul(a.c1, c2))), fq2_mul(a.c0, c0))));
+    return mk6(fq2_mul(t, c0), fq2_mul(t, c1), fq2_mul(t, c2));
+}
+
+// Frobenius coefficients (internal form, generated from fq6.rs:5-90 / fq12.rs:6-48)
+BN_INLINE Fq2<1> fq2_const(const Limbs9& c0, const Limbs9& c1) { return {fq_from_limbs<1>(c0), fq_from_limbs<1>(c1)}; }
+BN_INLINE Fq2<1> fq6_frob_c1(int n) {
+    if (n == 1) return fq2_const(Limbs9{BN_FQ6_C1_1_C0}, Limbs9{BN_FQ6_C1_1_C1});
+    if (n == 2) return fq2_const(Limbs9{BN_FQ6_C1_2_C0}, Limbs9{BN_FQ6_C1_2_C1});
+    return fq2_const(Limbs9{BN_FQ6_C1_3_C0}, Limbs9{BN_FQ6_C1_3_C1});
+}
+BN_INLINE Fq2<1> fq6_frob_c2(int n) {
+    if (n == 1) return fq2_const(Limbs9{BN_FQ6_C2_1_C0}, Limbs9{BN_FQ6_C2_1_C1});
+    if (n == 2) return fq2_const(Limbs9{BN_FQ6_C2_2_C0}, Limbs9{BN_FQ6_C2_2_C1});
+    return fq2_const(Limbs9{BN_FQ6_C2_3_C0}, Limbs9{BN_FQ6_C2_3_C1});
+}
+BN_INLINE Fq2<1> fq12_frob_c1(int n) {
+    if (n == 1) return fq2_const(Limbs9{BN_FQ12_C1_1_C0}, Limbs9{BN_FQ12_C1_1_C1});
+    if (n == 2) return fq2_const(Limbs9{BN_FQ12_C1_2_C0}, Limbs9{BN_FQ12_C1_2_C1});
+    return fq2_const(Limbs9{BN_FQ12_C1_3_C0}, Limbs9{BN_FQ12_C1_3_C1});
+}
+// fq6.rs:125-131 for power 1..3; power 2 coefficients are real (c1 == 0): two Fq products
+template <int POWER, int B>
+BN_INLINE auto fq6_frobenius_map(const Fq6<B>& a) {
+    if constexpr (POWER == 2) {
+        return mk6(a.c0, fq2_scale(a.c1, fq6_frob_c1(2).c0), fq2_scale(a.c2, fq6_frob_c2(2).c0));
+    } else {
+        return mk6(fq2_conj(a.c0), fq2_mul(fq2_conj(a.c1), fq6_frob_c1(POWER)), fq2_mul(fq2_conj(a.c2), fq6_frob_c2(POWER)));
+    }
+}
+
+// ================================================================ Fq12 = Fq6[w]/(w^2 - v)
+template <int A, int B>
+BN_INLINE Fq12<cmax(A, B)> mk12(const Fq6<A>& x, const Fq6<B>& y) {
+    return {widen<cmax(A, B)>(x), widen<cmax(A, B)>(y)};
+}
+template <int B2, int B>
+BN_INLINE Fq12<B2> widen(const Fq12<B>& a) { return {widen<B2>(a.c0), widen<B2>(a.c1)}; }
+BN_INLINE Fq12<1> fq12_one() { return {fq6_one(), fq6_zero()}; }
+template <int B>
+BN_INLINE Fq12<2> fq12_fold(const Fq12<B>& a) { return {fq6_fold(a.c0), fq6_fold(a.c1)}; }
+template <int B>
+BN_INLINE bool fq12_is_zero(const Fq12<B>& a) { return fq6_is_zero(a.c0) & fq6_is_zero(a.c1); }
+template <int L, int B>
+BN_INLINE auto pre(const Fq12<B>& a) {
+    if constexpr (B <= L) return a; else return fq12_fold(a);
+}
+template <int B>
+BN_INLINE Fq12<B> fq12_conj(const Fq12<B>& a) { return {a.c0, fq6_neg(a.c1)}; }  // unitary_inverse, fq12.rs:126-128
+template <int A, int B>
+BN_INLINE Fq12<A + B> fq12_add(const Fq12<A>& a, const Fq12<B>& b) { return {fq6_add(a.c0, b.c0), fq6_add(a.c1, b.c1)}; }
+template <int A, int B>
+BN_INLINE Fq12<A + B> fq12_sub(const Fq12<A>& a, const Fq12<B>& b) { return {fq6_sub(a.c0, b.c0), fq6_sub(a.c1, b.c1)}; }
+template <int B>
+BN_INLINE Fq12<B> fq12_neg(const Fq12<B>& a) { return {fq6_neg(a.c0), fq6_neg(a.c1)}; }
+
+// fq12.rs:319-327
+template <int A, int B>
+BN_INLINE auto fq12_mul(const Fq12<A>& a, const Fq12<B>& b) {
+    if constexpr (A > 10 || B > 10) return fq12_mul(pre<10>(a), pre<10>(b)); else {
+    auto aa = fq6_fold(fq6_mul(a.c0, b.c0));
+    auto bb = fq6_fold(fq6_mul(a.c1, b.c1));
+    auto t = fq6_mul(fq6_add(a.c0, a.c1), fq6_add(b.c0, b.c1));
+    return mk12(fq6_add(fq6_mul_by_nonresidue(bb), aa), fq6_sub(fq6_sub(t, aa), bb));
+    }
+}
+// fq12.rs:295-303
+template <int A>
+BN_INLINE auto fq12_sqr(const Fq12<A>& a) {
+    if constexpr (A > 2) return fq12_sqr(fq12_fold(a)); else {
+    auto ab = fq6_fold(fq6_mul(a.c0, a.c1));
+    auto t = fq6_mul(fq6_add(fq6_mul_by_nonresidue(a.c1), a.c0), fq6_add(a.c0, a.c1));
+    return mk12(fq6_sub(fq6_sub(t, ab), fq6_mul_by_nonresidue(ab)), fq6_add(ab, ab));
+    }
+}
+// fq12.rs:305-313
+template <int B>
+BN_INLINE auto fq12_inv(const Fq12<B>& a_in) {
+    auto a = fq12_fold(a_in);
+    auto t = fq6_inv(fq6_sub(fq6_fold(fq6_sqr(a.c0)), fq6_mul_by_nonresidue(fq6_fold(fq6_sqr(a.c1)))));
+    return mk12(fq6_mul(a.c0, t), fq6_neg(fq6_mul(a.c1, t)));
+}
+// fq12.rs:112-119
+template <int POWER, int B>
+BN_INLINE auto fq12_frobenius_map(const Fq12<B>& a) {
+    auto c1 = fq6_frobenius_map<POWER>(a.c1);
+    Fq2<1> k = fq12_frob_c1(POWER);
+    if constexpr (POWER == 2) {
+        return mk12(fq6_frobenius_map<POWER>(a.c0), mk6(fq2_scale(c1.c0, k.c0), fq2_scale(c1.c1, k.c0), fq2_scale(c1.c2, k.c0)));
+    } else {
+        return mk12(fq6_frobenius_map<POWER>(a.c0), mk6(fq2_mul(c1.c0, k), fq2_mul(c1.c1, k), fq2_mul(c1.c2, k)));
+    }
+}
+
+// fq12.rs:130-196 -- sparse product with a line (slots 0, 2, 4 nonzero)
+template <int F, int X>
+BN_INLINE auto fq12_mul_by_024(const Fq12<F>& f, const Fq2<X>& ell_0, const Fq2<X>& ell_vw, const Fq2<X>& ell_vv) {
+    const auto& z0 = f.c0.c0;
+    const auto& z1 = f.c0.c1;
+    const auto& z2 = f.c0.c2;
+    const auto& z3 = f.c1.c0;
+    const auto& z4 = f.c1.c1;
+    const auto& z5 = f.c1.c2;
+    const auto& x0 = ell_0;
+    const auto& x2 = ell_vv;
+    const auto& x4 = ell_vw;
+
+    auto d0 = fq2_mul(z0, x0);
+    auto d2 = fq2_mul(z2, x2);
+    auto d4 = fq2_mul(z4, x4);
+    auto t2 = fq2_add(z0, z4);
+    auto t1 = fq2_add(z0, z2);
+    auto s0 = fq2_add(fq2_add(z1, z3), z5);
+
+    auto s1a = fq2_mul(z1, x2);
+    auto n0 = fq2_add(fq2_mul_xi(fq2_add(s1a, d4)), d0);
+
+    auto t3a = fq2_mul(z5, x4);
+    auto s1b = fq2_add(s1a, t3a);
+    auto t4a = fq2_mul_xi(fq2_add(t3a, d2));
+    auto t3b = fq2_mul(z1, x0);
+    auto s1c = fq2_add(s1b, t3b);
+    auto n1 = fq2_add(t4a, t3b);
+
+    auto t3c = fq2_sub(fq2_sub(fq2_mul(t1, fq2_add(x0, x2)), d0), d2);
+    auto t4b = fq2_mul(z3, x4);
+    auto s1d = fq2_add(s1c, t4b);
+    auto n2 = fq2_add(t3c, t4b);
+
+    auto t3d = fq2_sub(fq2_sub(fq2_mul(fq2_add(z2, z4), fq2_add(x2, x4)), d2), d4);
+    auto t4c = fq2_mul_xi(t3d);
+    auto t3e = fq2_mul(z3, x0);
+    auto s1e = fq2_fold(fq2_add(s1d, t3e));
+    auto n3 = fq2_add(t4c, t3e);
+
+    auto t3f = fq2_mul(z5, x2);
+    auto s1f = fq2_add(s1e, t3f);
+    auto t4d = fq2_mul_xi(t3f);
+    auto t3g = fq2_sub(fq2_sub(fq2_mul(t2, fq2_add(x0, x4)), d0), d4);
+    auto n4 = fq2_add(t4d, t3g);
+
+    auto n5 = fq2_sub(fq2_mul(s0, fq2_add(fq2_add(x0, x2), x4)), s1f);
+    return mk12(mk6(n0, n1, n2), mk6(n3, n4, n5));
+}
+
+// fq12.rs:198-247 -- Granger-Scott cyclotomic squaring (the reference's formula)
+template <int A>
+BN_INLINE auto fq12_cyclotomic_sqr(const Fq12<A>& a) {
+    const auto& z0 = a.c0.c0;
+    const auto& z4 = a.c0.c1;
+    const auto& z3 = a.c0.c2;
+    const auto& z2 = a.c1.c0;
+    const auto& z1 = a.c1.c1;
+    const auto& z5 = a.c1.c2;
+    auto tmp01 = fq2_mul(z0, z1);
+    auto t0 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z0, z1), fq2_add(fq2_mul_xi(z1), z0)), tmp01), fq2_mul_xi(tmp01)));
+    auto t1 = fq2_dbl(tmp01);
+    auto tmp23 = fq2_mul(z2, z3);
+    auto t2 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z2, z3), fq2_add(fq2_mul_xi(z3), z2)), tmp23), fq2_mul_xi(tmp23)));
+    auto t3 = fq2_dbl(tmp23);
+    auto tmp45 = fq2_mul(z4, z5);
+    auto t4 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z4, z5), fq2_add(fq2_mul_xi(z5), z4)), tmp45), fq2_mul_xi(tmp45)));
+    auto t5 = fq2_dbl(tmp45);
+
+    auto n0 = fq2_add(fq2_dbl(fq2_sub(t0, z0)), t0);
+    auto n1 = fq2_add(fq2_dbl(fq2_add(t1, z1)), t1);
+    auto x5 = fq2_fold(fq2_mul_xi(t5));
+    auto n2 = fq2_add(fq2_dbl(fq2_add(x5, z2)), x5);
+    auto n3 = fq2_add(fq2_dbl(fq2_sub(t4, z3)), t4);
+    auto n4 = fq2_add(fq2_dbl(fq2_sub(t2, z4)), t2);
+    auto n5 = fq2_add(fq2_dbl(fq2_add(t3, z5)), t3);
+    return mk12(mk6(n0, n4, n3), mk6(n2, n1, n5));
+}
+
+}  // namespace bn
