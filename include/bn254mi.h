@@ -1,0 +1,110 @@
+/*
+ * bn254mi.h -- C ABI of the MI355X BN254 pairing engine (libbn254mi.so).
+ *
+ * Drop-in boundary for the batched hot path of risc0/paritytech-bn
+ * (crate substrate-bn 0.6.0).  The reference has no FFI; its boundary is the
+ * public Rust API in src/lib.rs.  Each entry point below names the reference
+ * function it replaces (file:line under /root/reference).  INTEGRATION.md shows
+ * the Rust-side `extern "C"` binding a maintainer adds to keep
+ * `pairing()/pairing_batch()/miller_loop_batch()/G1 * Fr` source-compatible.
+ *
+ * Value types are byte-identical to the reference's #[repr(C)] memory images,
+ * so Rust slices pass zero-copy:
+ *   bn_fq  == fields::Fq  == U256([u128;2]) : canonical x*2^256 mod p, little endian
+ *   bn_fr  == fields::Fr  (Montgomery mod r, same layout)
+ *   bn_g1  == groups::G1  == G<G1Params>{x,y,z}  (Jacobian; zero is z == 0)
+ *   bn_g2  == groups::G2  (Jacobian over Fq2 {c0,c1})
+ *   bn_gt  == Gt(Fq12)    12 Fq in order c0.c0.c0, c0.c0.c1, c0.c1.c0, ... c1.c2.c1
+ *
+ * Every call returns BN_OK (0) or a bn_status code.  Host-buffer calls block
+ * until the result is in the caller's buffer (the Rust API is synchronous).
+ * *_dev calls take device pointers and enqueue on `stream` (a hipStream_t, or
+ * NULL for the context's own stream) without synchronizing.
+ */
+#ifndef BN254MI_H
+#define BN254MI_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { uint64_t l[4]; } bn_fq;
+typedef struct { bn_fq c0, c1; } bn_fq2;
+typedef struct { uint64_t l[4]; } bn_fr;
+typedef struct { bn_fq x, y, z; } bn_g1;
+typedef struct { bn_fq2 x, y, z; } bn_g2;
+typedef struct { bn_fq c[12]; } bn_gt;
+
+typedef enum {
+    BN_OK = 0,
+    BN_ERR_INVALID_ARGUMENT = 1,
+    BN_ERR_TO_AFFINE = 2,     /* CurveError::ToAffineConversion (lib.rs:629-630) */
+    BN_ERR_FE_ZERO = 3,       /* final exponentiation of zero: fq12.rs:63-72 None; pairing panics (mod.rs:900) */
+    BN_ERR_HIP = 4,           /* a HIP runtime error; see bn_last_error() */
+    BN_ERR_NO_DEVICE = 5
+} bn_status;
+
+typedef struct bn_ctx bn_ctx;
+
+/* one context per device; calls on one context are serialized internally */
+int bn_ctx_create(int device, bn_ctx** out);
+int bn_ctx_destroy(bn_ctx* ctx);
+const char* bn_last_error(const bn_ctx* ctx);
+/* the stream *_dev calls use when given NULL */
+void* bn_ctx_stream(bn_ctx* ctx);
+
+/* ---- pairing path (src/groups/mod.rs:894-926, src/lib.rs:611-633) ---- */
+
+/* out[i] = pairing(p[i], q[i]) for i < n                     (lib.rs:611-613, mod.rs:894-902)
+ * Zero input point -> Gt::one().  BN_ERR_FE_ZERO if a Miller value is 0 (the reference panics). */
+int bn_pairing_many(bn_ctx* ctx, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out);
+int bn_pairing_many_dev(bn_ctx* ctx, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, void* stream);
+
+/* *out = pairing_batch(&[(p[i], q[i])])                       (lib.rs:615-623, mod.rs:904-926)
+ * Pairs with a zero point are skipped; n == 0 or all skipped -> Gt::one(). */
+int bn_pairing_batch(bn_ctx* ctx, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out);
+
+/* *out = miller_loop_batch(&[(q[i], p[i])]) -- note the (G2, G1) order (lib.rs:625-633,
+ * mod.rs:609-640).  No final exponentiation.  BN_ERR_TO_AFFINE if any point is zero. */
+int bn_miller_loop_batch(bn_ctx* ctx, const bn_g2* q, const bn_g1* p, size_t n, bn_gt* out);
+
+/* out[i] = Gt::final_exponentiation(f[i]) (lib.rs:598-600, fq12.rs:107-110);
+ * ok[i] = 0 where f[i] == 0 (the reference returns None), out[i] then zero. */
+int bn_final_exponentiation_many(bn_ctx* ctx, const bn_gt* f, size_t n, bn_gt* out, uint8_t* ok);
+
+/* per-pair Miller values G2Precomp::miller_loop (mod.rs:579-607) after to_affine +
+ * precompute; a pair with a zero point gives Fq12::one() */
+int bn_miller_loop_many(bn_ctx* ctx, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out);
+
+/* ---- group path (src/groups/mod.rs:250-334, lib.rs:425-431) ---- */
+
+/* out[i] = p[i] * k[i]: the reference's double-and-add chain (mod.rs:272-292), so the
+ * Jacobian output is bit-identical, not merely an equal point. */
+int bn_g1_mul_many(bn_ctx* ctx, const bn_g1* p, const bn_fr* k, size_t n, bn_g1* out);
+int bn_g1_mul_many_dev(bn_ctx* ctx, const bn_g1* d_p, const bn_fr* d_k, size_t n, bn_g1* d_out, void* stream);
+int bn_g2_mul_many(bn_ctx* ctx, const bn_g2* p, const bn_fr* k, size_t n, bn_g2* out);
+int bn_g2_mul_many_dev(bn_ctx* ctx, const bn_g2* d_p, const bn_fr* d_k, size_t n, bn_g2* d_out, void* stream);
+
+/* ---- Gt / Fq12 element operations (src/fields/fq12.rs) for batched callers and tests ---- */
+typedef enum {
+    BN_FQ12_MUL = 0,          /* a * b          fq12.rs:319-327 (Gt * Gt, lib.rs:603-609) */
+    BN_FQ12_SQR = 1,          /* a^2            fq12.rs:295-303 */
+    BN_FQ12_INV = 2,          /* a^-1 (0 -> 0)  fq12.rs:305-313 */
+    BN_FQ12_CYC_SQR = 3,      /* cyclotomic_squared fq12.rs:198-247 */
+    BN_FQ12_EXP_BY_NEG_Z = 4, /* fq12.rs:121-124 */
+    BN_FQ12_FROB1 = 5, BN_FQ12_FROB2 = 6, BN_FQ12_FROB3 = 7 /* fq12.rs:112-119 */
+} bn_fq12_op;
+int bn_fq12_op_many(bn_ctx* ctx, int op, const bn_gt* a, const bn_gt* b, size_t n, bn_gt* out);
+
+/* ---- workspace ---- */
+/* device bytes the context holds for a batch of n pairings (allocated on first use) */
+size_t bn_workspace_bytes(size_t n);
+/* pre-size the context workspace for batches up to n (avoids allocation inside timed loops) */
+int bn_reserve(bn_ctx* ctx, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

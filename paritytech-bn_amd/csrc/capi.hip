@@ -1,0 +1,495 @@
+// capi.hip -- host side of the C ABI (include/bn254mi.h): context, workspace,
+// chunking, the final-exponentiation step program, and kernel launches.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+
+using namespace bn;
+
+// ================================================================ host side
+struct bn_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string err;
+    // workspace (device)
+    size_t cap = 0;  // pairings
+    uint32_t* coeffs = nullptr;
+    uint32_t* paff = nullptr;
+    uint32_t* slots = nullptr;  // Fq12 slots of the step machine; slot 0 = Miller values
+    uint8_t* flags = nullptr;
+    uint32_t* d_prog = nullptr; // final-exponentiation step program
+    int fe_steps = 0;
+    int fe_out = 0;
+    int* d_err = nullptr;
+    // staging for host-buffer calls (device)
+    size_t stage_bytes = 0;
+    void* stage = nullptr;
+};
+
+namespace {
+
+int fail(bn_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+#define HIPCHK(ctx, x)                                                                   \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess)                                                            \
+            return fail(ctx, BN_ERR_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kFeSlots = 32;  // slot 0: Miller value, 1: easy-part result, 2..: temporaries
+
+size_t ws_bytes(size_t n) {
+    return n * ((size_t)kCoeffFq * 9 * 4 + 2 * 9 * 4 + (size_t)kFeSlots * kSlotWords * 4 + 1) + 64;
+}
+
+// ---------------------------------------------------------------- FE step program
+struct Prog {
+    std::vector<uint32_t> s;
+    uint32_t next = 2;
+    uint32_t tmp() { return next++; }
+    void op(Fq12Op o, uint32_t d, uint32_t a, uint32_t b = 0) { s.push_back(vm_step(o, d, a, b)); }
+    // exp_by_neg_z, fq12.rs:121-124 + cyclotomic_pow fq12.rs:249-266 (u = 0x44e992b44a6909f1)
+    uint32_t exp_by_neg_z(uint32_t x) {
+        const uint64_t u = 4965661367192848881ull;
+        const uint32_t r = tmp();
+        op(OP_MOV, r, x);  // first set bit (62): one * x
+        for (int bit = 61; bit >= 0; --bit) {
+            op(OP_CYC, r, r);
+            if ((u >> bit) & 1) op(OP_MUL, r, x, r);
+        }
+        op(OP_CONJ, r, r);
+        return r;
+    }
+};
+// final_exponentiation (fq12.rs:107-110) of slot 0; returns the result slot
+uint32_t build_final_exp(Prog& P) {
+    // first chunk, fq12.rs:62-73
+    const uint32_t b = P.tmp(), a = P.tmp(), c = P.tmp(), d = P.tmp();
+    P.op(OP_INV, b, 0);
+    P.op(OP_CONJ, a, 0);
+    P.op(OP_MUL, c, a, b);
+    P.op(OP_FROB2, d, c);
+    P.op(OP_MUL, 1, d, c);  // slot 1 = self of the last chunk
+    // last chunk, fq12.rs:75-105
+    const uint32_t A = P.exp_by_neg_z(1);
+    const uint32_t B = P.tmp(), C = P.tmp(), D = P.tmp();
+    P.op(OP_CYC, B, A);
+    P.op(OP_CYC, C, B);
+    P.op(OP_MUL, D, C, B);
+    const uint32_t E = P.exp_by_neg_z(D);
+    const uint32_t F = P.tmp();
+    P.op(OP_CYC, F, E);
+    const uint32_t G = P.exp_by_neg_z(F);
+    const uint32_t H = P.tmp(), I = P.tmp(), J = P.tmp(), K = P.tmp(), L = P.tmp(), M = P.tmp(), N = P.tmp();
+    P.op(OP_CONJ, H, D);
+    P.op(OP_CONJ, I, G);
+    P.op(OP_MUL, J, I, E);
+    P.op(OP_MUL, K, J, H);
+    P.op(OP_MUL, L, K, B);
+    P.op(OP_MUL, M, K, E);
+    P.op(OP_MUL, N, 1, M);
+    const uint32_t O = P.tmp(), Pp = P.tmp(), Q = P.tmp(), R = P.tmp(), S = P.tmp(), T = P.tmp(), U = P.tmp(),
+                   V = P.tmp();
+    P.op(OP_FROB1, O, L);
+    P.op(OP_MUL, Pp, O, N);
+    P.op(OP_FROB2, Q, K);
+    P.op(OP_MUL, R, Q, Pp);
+    P.op(OP_CONJ, S, 1);
+    P.op(OP_MUL, T, S, L);
+    P.op(OP_FROB3, U, T);
+    P.op(OP_MUL, V, U, R);
+    return V;
+}
+
+int reserve(bn_ctx* c, size_t n) {
+    if (n <= c->cap) return BN_OK;
+    n = n < 1024 ? 1024 : n;
+    if (c->coeffs) hipFree(c->coeffs);
+    if (c->paff) hipFree(c->paff);
+    if (c->slots) hipFree(c->slots);
+    if (c->flags) hipFree(c->flags);
+    c->coeffs = nullptr; c->paff = nullptr; c->slots = nullptr; c->flags = nullptr; c->cap = 0;
+    HIPCHK(c, hipMalloc(&c->coeffs, n * (size_t)kCoeffFq * 9 * 4));
+    HIPCHK(c, hipMalloc(&c->paff, n * 2 * 9 * 4));
+    HIPCHK(c, hipMalloc(&c->slots, n * (size_t)kFeSlots * kSlotWords * 4));
+    HIPCHK(c, hipMalloc(&c->flags, n));
+    c->cap = n;
+    return BN_OK;
+}
+int stage(bn_ctx* c, size_t bytes) {
+    if (bytes <= c->stage_bytes) return BN_OK;
+    if (c->stage) hipFree(c->stage);
+    c->stage = nullptr;
+    c->stage_bytes = 0;
+    HIPCHK(c, hipMalloc(&c->stage, bytes));
+    c->stage_bytes = bytes;
+    return BN_OK;
+}
+hipStream_t pick(bn_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+// Miller values of n pairs into slot 0 (lane-strided, stride = n); n <= c->cap
+int miller_values(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int mode, hipStream_t s) {
+    k_prepare<<<grid_for(n), kBlock, 0, s>>>(d_p, d_q, n, c->coeffs, c->paff, c->flags, c->d_err, mode);
+    HIPCHK(c, hipGetLastError());
+    k_miller<<<grid_for(n), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, n, c->slots);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+// multiply the n lane-strided values of slot 0 together into lane 0
+int product_tree(bn_ctx* c, size_t n, hipStream_t s) {
+    for (size_t m = n; m > 1;) {
+        const size_t half = (m + 1) / 2;
+        k_fq12_product<<<grid_for(half), kBlock, 0, s>>>(c->slots, n, m, half);
+        HIPCHK(c, hipGetLastError());
+        m = half;
+    }
+    return BN_OK;
+}
+
+// final exponentiation of the n values in slot 0 -> out (device Gt images)
+int run_fe(bn_ctx* c, size_t n, const uint8_t* flags, bn_gt* out, uint8_t* ok, hipStream_t s) {
+    k_fq12_vm<<<grid_for(n), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, n);
+    HIPCHK(c, hipGetLastError());
+    k_fe_out<<<grid_for(n), kBlock, 0, s>>>(c->slots, n, c->fe_out, flags, out, ok, c->d_err);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+
+int check_err(bn_ctx* c, hipStream_t s, int* out_bits) {
+    int h = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, c->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    *out_bits = h;
+    return BN_OK;
+}
+int clear_err(bn_ctx* c, hipStream_t s) {
+    HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), s));
+    return BN_OK;
+}
+
+}  // namespace
+
+#define CTX_GUARD(ctx)                                 \
+    if (!(ctx)) return BN_ERR_INVALID_ARGUMENT;        \
+    std::lock_guard<std::mutex> lock_((ctx)->mu);      \
+    HIPCHK(ctx, hipSetDevice((ctx)->device))
+#define RET_IF(x)              \
+    do {                       \
+        int r_ = (x);          \
+        if (r_) return r_;     \
+    } while (0)
+
+template <typename P, typename K>
+static int host_mul(bn_ctx* c, const P* p, const bn_fr* k, size_t n, P* out, K kernel) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!p || !k || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    RET_IF(stage(c, n * (2 * sizeof(P) + sizeof(bn_fr))));
+    P* dp = (P*)c->stage;
+    P* dout = dp + n;
+    bn_fr* dk = (bn_fr*)(dout + n);
+    HIPCHK(c, hipMemcpyAsync(dp, p, n * sizeof(P), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dk, k, n * sizeof(bn_fr), hipMemcpyHostToDevice, c->stream));
+    kernel<<<grid_for(n), kBlock, 0, c->stream>>>(dp, dk, n, dout);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(out, dout, n * sizeof(P), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BN_OK;
+}
+
+extern "C" {
+
+int bn_ctx_create(int device, bn_ctx** out) {
+    if (!out) return BN_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return BN_ERR_NO_DEVICE;
+    if (device < 0 || device >= count) return BN_ERR_INVALID_ARGUMENT;
+    bn_ctx* c = new bn_ctx();
+    c->device = device;
+    Prog P;
+    c->fe_out = (int)build_final_exp(P);
+    c->fe_steps = (int)P.s.size();
+    if (P.next > (uint32_t)kFeSlots) {
+        delete c;
+        return BN_ERR_INVALID_ARGUMENT;
+    }
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess ||
+        hipMalloc(&c->d_prog, P.s.size() * 4) != hipSuccess ||
+        hipMemcpy(c->d_prog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        delete c;
+        return BN_ERR_HIP;
+    }
+    *out = c;
+    return BN_OK;
+}
+
+int bn_ctx_destroy(bn_ctx* c) {
+    if (!c) return BN_ERR_INVALID_ARGUMENT;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (void* p : {(void*)c->coeffs, (void*)c->paff, (void*)c->slots, (void*)c->flags, (void*)c->d_err,
+                    (void*)c->d_prog, c->stage})
+        if (p) hipFree(p);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return BN_OK;
+}
+
+const char* bn_last_error(const bn_ctx* c) { return c ? c->err.c_str() : "null context"; }
+void* bn_ctx_stream(bn_ctx* c) { return c ? (void*)c->stream : nullptr; }
+size_t bn_workspace_bytes(size_t n) { return ws_bytes(n); }
+
+int bn_reserve(bn_ctx* c, size_t n) {
+    CTX_GUARD(c);
+    return reserve(c, n < kChunk ? n : kChunk);
+}
+
+int bn_pairing_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, void* stream) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!d_p || !d_q || !d_out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    hipStream_t s = pick(c, stream);
+    RET_IF(reserve(c, n < kChunk ? n : kChunk));
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        RET_IF(miller_values(c, d_p + off, d_q + off, m, 0, s));
+        RET_IF(run_fe(c, m, c->flags, d_out + off, nullptr, s));
+    }
+    return BN_OK;
+}
+
+int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
+    if (!c) return BN_ERR_INVALID_ARGUMENT;
+    if (n == 0) return BN_OK;
+    if (!p || !q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        bn_g1* dp;
+        bn_g2* dq;
+        bn_gt* dout;
+        {
+            CTX_GUARD(c);
+            RET_IF(stage(c, m * (sizeof(bn_g1) + sizeof(bn_g2) + sizeof(bn_gt))));
+            dp = (bn_g1*)c->stage;
+            dq = (bn_g2*)(dp + m);
+            dout = (bn_gt*)(dq + m);
+            RET_IF(clear_err(c, c->stream));
+            HIPCHK(c, hipMemcpyAsync(dp, p + off, m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
+        }
+        RET_IF(bn_pairing_many_dev(c, dp, dq, m, dout, nullptr));
+        CTX_GUARD(c);
+        HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
+        int bits = 0;
+        RET_IF(check_err(c, c->stream, &bits));
+        if (bits & (1 << BN_ERR_FE_ZERO)) return fail(c, BN_ERR_FE_ZERO, "miller loop cannot produce zero");
+    }
+    return BN_OK;
+}
+
+// product of the Miller values of all pairs (mode 0: pairs with a zero point
+// contribute one; mode 1: a zero point is BN_ERR_TO_AFFINE) -> *result (host image)
+static int miller_product(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, int mode, bn_gt* result) {
+    RET_IF(clear_err(c, c->stream));
+    std::vector<bn_gt> parts;
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        RET_IF(stage(c, m * (sizeof(bn_g1) + sizeof(bn_g2)) + sizeof(bn_gt)));
+        bn_g1* dp = (bn_g1*)c->stage;
+        bn_g2* dq = (bn_g2*)(dp + m);
+        bn_gt* dpart = (bn_gt*)(dq + m);
+        HIPCHK(c, hipMemcpyAsync(dp, p + off, m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
+        RET_IF(reserve(c, m));
+        RET_IF(miller_values(c, dp, dq, m, mode, c->stream));
+        RET_IF(product_tree(c, m, c->stream));
+        k_gt_store<<<1, kBlock, 0, c->stream>>>(c->slots, 1, m, dpart);
+        HIPCHK(c, hipGetLastError());
+        bn_gt h;
+        HIPCHK(c, hipMemcpyAsync(&h, dpart, sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        parts.push_back(h);
+    }
+    int bits = 0;
+    RET_IF(check_err(c, c->stream, &bits));
+    if (bits & (1 << BN_ERR_TO_AFFINE)) return fail(c, BN_ERR_TO_AFFINE, "ToAffineConversion");
+    if (parts.size() == 1) {
+        *result = parts[0];
+        return BN_OK;
+    }
+    const size_t np = parts.size();
+    RET_IF(stage(c, (np + 1) * sizeof(bn_gt)));
+    bn_gt* d = (bn_gt*)c->stage;
+    HIPCHK(c, hipMemcpyAsync(d, parts.data(), np * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
+    RET_IF(reserve(c, np));
+    k_gt_load<<<grid_for(np), kBlock, 0, c->stream>>>(d, np, c->slots);
+    RET_IF(product_tree(c, np, c->stream));
+    k_gt_store<<<1, kBlock, 0, c->stream>>>(c->slots, 1, np, d + np);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(result, d + np, sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BN_OK;
+}
+
+static void gt_one(bn_gt* out) {  // Fq12::one() image: c0.c0.c0 = R mod p
+    memset(out, 0, sizeof(bn_gt));
+    out->c[0].l[0] = 0xd35d438dc58f0d9dull;
+    out->c[0].l[1] = 0x0a78eb28f5c70b3dull;
+    out->c[0].l[2] = 0x666ea36f7879462cull;
+    out->c[0].l[3] = 0x0e0a77c19a07df2full;
+}
+
+// final exponentiation of n host images; ok may be null
+static int final_exp_host(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8_t* ok, int* zero_seen) {
+    *zero_seen = 0;
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        RET_IF(reserve(c, m));
+        RET_IF(stage(c, m * (2 * sizeof(bn_gt) + 1)));
+        bn_gt* din = (bn_gt*)c->stage;
+        bn_gt* dout = din + m;
+        uint8_t* dok = (uint8_t*)(dout + m);
+        HIPCHK(c, hipMemcpyAsync(din, f + off, m * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
+        k_gt_load<<<grid_for(m), kBlock, 0, c->stream>>>(din, m, c->slots);
+        HIPCHK(c, hipGetLastError());
+        RET_IF(run_fe(c, m, nullptr, dout, dok, c->stream));
+        HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
+        if (ok) HIPCHK(c, hipMemcpyAsync(ok + off, dok, m, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    int bits = 0;
+    RET_IF(check_err(c, c->stream, &bits));
+    *zero_seen = (bits & (1 << BN_ERR_FE_ZERO)) != 0;
+    return BN_OK;
+}
+
+int bn_pairing_batch(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
+    CTX_GUARD(c);
+    if (!out || (n && (!p || !q))) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    if (n == 0) {  // mod.rs:922-924
+        gt_one(out);
+        return BN_OK;
+    }
+    bn_gt prod;
+    RET_IF(miller_product(c, p, q, n, 0, &prod));
+    RET_IF(clear_err(c, c->stream));
+    int zero = 0;
+    RET_IF(final_exp_host(c, &prod, 1, out, nullptr, &zero));
+    if (zero) return fail(c, BN_ERR_FE_ZERO, "miller loop cannot produce zero");
+    return BN_OK;
+}
+
+int bn_miller_loop_batch(bn_ctx* c, const bn_g2* q, const bn_g1* p, size_t n, bn_gt* out) {
+    CTX_GUARD(c);
+    if (!out || (n && (!p || !q))) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    if (n == 0) {  // the shared loop starts from Fq12::one() (mod.rs:610)
+        gt_one(out);
+        return BN_OK;
+    }
+    return miller_product(c, p, q, n, 1, out);
+}
+
+int bn_final_exponentiation_many(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8_t* ok) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!f || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    RET_IF(clear_err(c, c->stream));
+    int zero = 0;
+    return final_exp_host(c, f, n, out, ok, &zero);
+}
+
+int bn_miller_loop_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!p || !q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        RET_IF(reserve(c, m));
+        RET_IF(stage(c, m * (sizeof(bn_g1) + sizeof(bn_g2) + sizeof(bn_gt))));
+        bn_g1* dp = (bn_g1*)c->stage;
+        bn_g2* dq = (bn_g2*)(dp + m);
+        bn_gt* dout = (bn_gt*)(dq + m);
+        HIPCHK(c, hipMemcpyAsync(dp, p + off, m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
+        RET_IF(miller_values(c, dp, dq, m, 0, c->stream));
+        k_gt_store<<<grid_for(m), kBlock, 0, c->stream>>>(c->slots, m, m, dout);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return BN_OK;
+}
+
+int bn_g1_mul_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_fr* d_k, size_t n, bn_g1* d_out, void* stream) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!d_p || !d_k || !d_out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    k_g1_mul<<<grid_for(n), kBlock, 0, pick(c, stream)>>>(d_p, d_k, n, d_out);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+int bn_g2_mul_many_dev(bn_ctx* c, const bn_g2* d_p, const bn_fr* d_k, size_t n, bn_g2* d_out, void* stream) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!d_p || !d_k || !d_out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    k_g2_mul<<<grid_for(n), kBlock, 0, pick(c, stream)>>>(d_p, d_k, n, d_out);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+int bn_g1_mul_many(bn_ctx* c, const bn_g1* p, const bn_fr* k, size_t n, bn_g1* out) { return host_mul(c, p, k, n, out, k_g1_mul); }
+int bn_g2_mul_many(bn_ctx* c, const bn_g2* p, const bn_fr* k, size_t n, bn_g2* out) { return host_mul(c, p, k, n, out, k_g2_mul); }
+
+int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n, bn_gt* out) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (op < 0 || op > BN_FQ12_FROB3) return fail(c, BN_ERR_INVALID_ARGUMENT, "bad op");
+    if (!a || !out || (op == BN_FQ12_MUL && !b)) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        RET_IF(reserve(c, m));
+        RET_IF(stage(c, m * 3 * sizeof(bn_gt) + 4096));
+        bn_gt* da = (bn_gt*)c->stage;
+        bn_gt* db = da + m;
+        bn_gt* dout = db + m;
+        uint32_t* dprog = (uint32_t*)(dout + m);
+        HIPCHK(c, hipMemcpyAsync(da, a + off, m * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
+        k_gt_load<<<grid_for(m), kBlock, 0, c->stream>>>(da, m, c->slots + (size_t)1 * kSlotWords * m);
+        if (op == BN_FQ12_MUL) {
+            HIPCHK(c, hipMemcpyAsync(db, b + off, m * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
+            k_gt_load<<<grid_for(m), kBlock, 0, c->stream>>>(db, m, c->slots + (size_t)2 * kSlotWords * m);
+        }
+        Prog P;
+        P.next = 3;
+        uint32_t res = P.tmp();
+        switch (op) {
+            case BN_FQ12_MUL: P.op(OP_MUL, res, 1, 2); break;
+            case BN_FQ12_SQR: P.op(OP_SQR, res, 1); break;
+            case BN_FQ12_INV: P.op(OP_INV, res, 1); break;
+            case BN_FQ12_CYC_SQR: P.op(OP_CYC, res, 1); break;
+            case BN_FQ12_EXP_BY_NEG_Z: res = P.exp_by_neg_z(1); break;
+            case BN_FQ12_FROB1: P.op(OP_FROB1, res, 1); break;
+            case BN_FQ12_FROB2: P.op(OP_FROB2, res, 1); break;
+            default: P.op(OP_FROB3, res, 1); break;
+        }
+        HIPCHK(c, hipMemcpyAsync(dprog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice, c->stream));
+        k_fq12_vm<<<grid_for(m), kBlock, 0, c->stream>>>(dprog, (int)P.s.size(), c->slots, m);
+        k_gt_store<<<grid_for(m), kBlock, 0, c->stream>>>(c->slots + (size_t)res * kSlotWords * m, m, m, dout);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return BN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,176 @@
+// kernels.h -- shared device helpers and the kernel declarations of the engine
+// (definitions in kernels_*.hip; launched from capi.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/bn254mi.h"
+#include "pairing.h"
+
+namespace bn {
+
+constexpr int kBlock = 64;               // one wave per workgroup: even spread over SIMDs
+constexpr int kCoeffFq = BN_NUM_COEFFS * 6;  // Fq elements of line coefficients per pairing
+constexpr size_t kChunk = size_t(1) << 18;   // pairings per launch set (~5 GB workspace)
+
+// ---------------------------------------------------------------- lane-strided storage
+template <int B>
+__device__ __forceinline__ void st_fq(uint32_t* base, size_t n, size_t i, int j, const Fq<B>& x) {
+#pragma unroll
+    for (int l = 0; l < 9; ++l) base[((size_t)j * 9 + l) * n + i] = x.v[l];
+}
+template <int B>
+__device__ __forceinline__ Fq<B> ld_fq(const uint32_t* base, size_t n, size_t i, int j) {
+    Fq<B> x;
+#pragma unroll
+    for (int l = 0; l < 9; ++l) x.v[l] = base[((size_t)j * 9 + l) * n + i];
+    return x;
+}
+template <int B>
+__device__ __forceinline__ void st_fq2(uint32_t* base, size_t n, size_t i, int j, const Fq2<B>& x) {
+    st_fq(base, n, i, j, x.c0);
+    st_fq(base, n, i, j + 1, x.c1);
+}
+template <int B>
+__device__ __forceinline__ Fq2<B> ld_fq2(const uint32_t* base, size_t n, size_t i, int j) {
+    return {ld_fq<B>(base, n, i, j), ld_fq<B>(base, n, i, j + 1)};
+}
+template <int B>
+__device__ __forceinline__ void st_fq12(uint32_t* base, size_t n, size_t i, const Fq12<B>& f) {
+    st_fq2(base, n, i, 0, f.c0.c0);
+    st_fq2(base, n, i, 2, f.c0.c1);
+    st_fq2(base, n, i, 4, f.c0.c2);
+    st_fq2(base, n, i, 6, f.c1.c0);
+    st_fq2(base, n, i, 8, f.c1.c1);
+    st_fq2(base, n, i, 10, f.c1.c2);
+}
+template <int B>
+__device__ __forceinline__ Fq12<B> ld_fq12(const uint32_t* base, size_t n, size_t i) {
+    return {{ld_fq2<B>(base, n, i, 0), ld_fq2<B>(base, n, i, 2), ld_fq2<B>(base, n, i, 4)},
+            {ld_fq2<B>(base, n, i, 6), ld_fq2<B>(base, n, i, 8), ld_fq2<B>(base, n, i, 10)}};
+}
+
+// ---------------------------------------------------------------- reference images
+__device__ __forceinline__ void ld_words(const bn_fq* src, uint32_t w[8]) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4 a = s[0], b = s[1];
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+__device__ __forceinline__ void st_words(bn_fq* dst, const uint32_t w[8]) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    d[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    d[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+__device__ __forceinline__ bool words_zero(const uint32_t w[8]) {
+    return (w[0] | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7]) == 0;
+}
+__device__ __forceinline__ Fq<2> ld_ref(const bn_fq& a) {
+    uint32_t w[8];
+    ld_words(&a, w);
+    return fq_load_ref(w);
+}
+template <int B>
+__device__ __forceinline__ void st_ref(bn_fq& a, const Fq<B>& x) {
+    uint32_t w[8];
+    fq_store_ref(x, w);
+    st_words(&a, w);
+}
+__device__ __forceinline__ Fq2<2> ld_ref2(const bn_fq2& a) { return {ld_ref(a.c0), ld_ref(a.c1)}; }
+template <int B>
+__device__ __forceinline__ void st_ref2(bn_fq2& a, const Fq2<B>& x) {
+    st_ref(a.c0, x.c0);
+    st_ref(a.c1, x.c1);
+}
+template <int B>
+__device__ __forceinline__ void st_gt(bn_gt& g, const Fq12<B>& f) {
+    const Fq2<B>* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        st_ref(g.c[2 * k], c[k]->c0);
+        st_ref(g.c[2 * k + 1], c[k]->c1);
+    }
+}
+__device__ __forceinline__ Fq12<2> ld_gt(const bn_gt& g) {
+    Fq2<2> c[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) c[k] = {ld_ref(g.c[2 * k]), ld_ref(g.c[2 * k + 1])};
+    return {{c[0], c[1], c[2]}, {c[3], c[4], c[5]}};
+}
+__device__ __forceinline__ void st_gt_zero(bn_gt& g) {
+    uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 12; ++k) st_words(&g.c[k], z);
+}
+
+// Fr Montgomery image -> canonical scalar words: U256::from(Fr), fp.rs:13-20
+// (one REDC by r with 32-bit digits; once per scalar product)
+__device__ __forceinline__ void fr_to_canonical(const bn_fr& k, uint32_t out[8]) {
+    constexpr uint32_t R[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                               0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+    uint32_t t[9];
+    ld_words(reinterpret_cast<const bn_fq*>(&k), t);
+    t[8] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t m = t[0] * 0xefffffffu;
+        uint64_t c = ((uint64_t)m * R[0] + t[0]) >> 32;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            const uint64_t s = (uint64_t)m * R[j] + t[j] + c;
+            t[j - 1] = (uint32_t)s;
+            c = s >> 32;
+        }
+        const uint64_t s = (uint64_t)t[8] + c;
+        t[7] = (uint32_t)s;
+        t[8] = (uint32_t)(s >> 32);
+    }
+    uint32_t d[8];
+    int64_t br = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int64_t s = (int64_t)t[j] - R[j] + br;
+        d[j] = (uint32_t)s;
+        br = s >> 32;
+    }
+    const bool ge = (t[8] != 0) || (br == 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = ge ? d[j] : t[j];
+}
+
+__device__ __forceinline__ size_t lane_id() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
+
+
+inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+// ---------------------------------------------------------------- Fq12 step machine
+// The final exponentiation is ~300 Fq12 operations; compiled inline it is one
+// enormous kernel (minutes to build, scratch spills).  Instead k_fq12_vm runs a
+// step program over lane-strided Fq12 slots in HBM: each step loads its
+// operands, computes in registers, stores the result.  Every operation's code
+// exists once; the operand traffic (<= 1.3 KB per lane per Fq12 product, which
+// itself takes ~50k cycles) is negligible.  The opcode is wave-uniform.
+enum Fq12Op : uint32_t {
+    OP_MOV = 0, OP_MUL = 1, OP_SQR = 2, OP_CYC = 3, OP_CONJ = 4,
+    OP_FROB1 = 5, OP_FROB2 = 6, OP_FROB3 = 7, OP_INV = 8
+};
+constexpr int kSlotWords = 108;  // 12 Fq x 9 digits
+inline uint32_t vm_step(uint32_t op, uint32_t d, uint32_t a, uint32_t b = 0) {
+    return op | (d << 8) | (a << 16) | (b << 24);
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ void __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
+                          uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
+                          int* __restrict__ err, int mode);
+__global__ void __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ coeffs, const uint32_t* __restrict__ paff,
+                         const uint8_t* __restrict__ flags, size_t n, uint32_t* __restrict__ f_out);
+__global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps, uint32_t* slots, size_t n);
+__global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot, const uint8_t* __restrict__ flags,
+                         bn_gt* __restrict__ out, uint8_t* __restrict__ ok, int* __restrict__ err);
+__global__ void __launch_bounds__(kBlock) k_fq12_product(uint32_t* __restrict__ f, size_t stride, size_t m, size_t half);
+__global__ void __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g, size_t n, uint32_t* __restrict__ f);
+__global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict__ f, size_t n, size_t stride, bn_gt* __restrict__ g);
+__global__ void __launch_bounds__(kBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g1* __restrict__ out);
+__global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g2* __restrict__ out);
+
+}  // namespace bn

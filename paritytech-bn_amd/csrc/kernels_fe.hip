@@ -1,0 +1,57 @@
+// kernels_fe.hip -- final exponentiation (fq12.rs:62-124, 249-266) as a step
+// program over lane-strided Fq12 slots (see kernels.h), plus the Gt output.
+#include "kernels.h"
+
+namespace bn {
+
+__device__ __forceinline__ uint32_t* slot_ptr(uint32_t* slots, size_t n, uint32_t s) {
+    return slots + (size_t)s * kSlotWords * n;
+}
+
+__global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps, uint32_t* slots,
+                                                    size_t n) {
+    const size_t i = lane_id();
+    if (i >= n) return;
+#pragma unroll 1
+    for (int pc = 0; pc < nsteps; ++pc) {
+        const uint32_t ins = prog[pc];  // uniform: scalar load
+        const uint32_t op = ins & 0xff;
+        uint32_t* d = slot_ptr(slots, n, (ins >> 8) & 0xff);
+        const uint32_t* a = slot_ptr(slots, n, (ins >> 16) & 0xff);
+        const uint32_t* b = slot_ptr(slots, n, ins >> 24);
+        switch (op) {
+            case OP_MOV: st_fq12(d, n, i, ld_fq12<kF>(a, n, i)); break;
+            case OP_MUL: st_fq12(d, n, i, mul12(ld_fq12<kF>(a, n, i), ld_fq12<kF>(b, n, i))); break;
+            case OP_SQR: st_fq12(d, n, i, narrow12<kF>(fq12_sqr(ld_fq12<kF>(a, n, i)))); break;
+            case OP_CYC: st_fq12(d, n, i, cyc_sqr(ld_fq12<kF>(a, n, i))); break;
+            case OP_CONJ: st_fq12(d, n, i, fq12_conj(ld_fq12<kF>(a, n, i))); break;
+            case OP_FROB1: st_fq12(d, n, i, narrow12<kF>(fq12_frobenius_map<1>(ld_fq12<kF>(a, n, i)))); break;
+            case OP_FROB2: st_fq12(d, n, i, narrow12<kF>(fq12_frobenius_map<2>(ld_fq12<kF>(a, n, i)))); break;
+            case OP_FROB3: st_fq12(d, n, i, narrow12<kF>(fq12_frobenius_map<3>(ld_fq12<kF>(a, n, i)))); break;
+            default: st_fq12(d, n, i, narrow12<kF>(fq12_inv(ld_fq12<kF>(a, n, i)))); break;  // OP_INV
+        }
+    }
+}
+
+// out[i] = slot `out_slot`; slot 0 holds the Miller value: f == 0 means the
+// reference returns None (fq12.rs:63-72) and pairing() panics -> zero Gt,
+// ok[i] = 0, error bit.  flags[i] (a zero input point) -> Fq12::one().
+__global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot,
+                                                   const uint8_t* __restrict__ flags, bn_gt* __restrict__ out,
+                                                   uint8_t* __restrict__ ok, int* __restrict__ err) {
+    const size_t i = lane_id();
+    if (i >= n) return;
+    const bool skip = flags && flags[i];
+    const bool zero = !skip && fq12_is_zero(ld_fq12<kF>(slots, n, i));
+    if (ok) ok[i] = zero ? 0 : 1;
+    if (zero) {
+        if (err) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        st_gt_zero(out[i]);
+    } else if (skip) {
+        st_gt(out[i], fq12_one());
+    } else {
+        st_gt(out[i], ld_fq12<kF>(slots + (size_t)out_slot * kSlotWords * n, n, i));
+    }
+}
+
+}  // namespace bn

@@ -1,0 +1,32 @@
+// kernels_group.hip -- batched G1/G2 scalar multiplication (mod.rs:272-292), one lane per product.
+#include "kernels.h"
+
+namespace bn {
+
+// ---------------------------------------------------------------- scalar multiplication
+__global__ void __launch_bounds__(kBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n,
+                                                   bn_g1* __restrict__ out) {
+    const size_t i = lane_id();
+    if (i >= n) return;
+    uint32_t s[8];
+    fr_to_canonical(k[i], s);
+    G1J a = {widen<kPt>(ld_ref(p[i].x)), widen<kPt>(ld_ref(p[i].y)), widen<kPt>(ld_ref(p[i].z))};
+    G1J r = jac_mul(a, s);
+    st_ref(out[i].x, r.x);
+    st_ref(out[i].y, r.y);
+    st_ref(out[i].z, r.z);
+}
+__global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n,
+                                                   bn_g2* __restrict__ out) {
+    const size_t i = lane_id();
+    if (i >= n) return;
+    uint32_t s[8];
+    fr_to_canonical(k[i], s);
+    G2J a = {widen<kPt>(ld_ref2(p[i].x)), widen<kPt>(ld_ref2(p[i].y)), widen<kPt>(ld_ref2(p[i].z))};
+    G2J r = jac_mul(a, s);
+    st_ref2(out[i].x, r.x);
+    st_ref2(out[i].y, r.y);
+    st_ref2(out[i].z, r.z);
+}
+
+}  // namespace bn

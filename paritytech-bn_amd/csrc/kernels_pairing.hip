@@ -1,0 +1,60 @@
+// kernels_pairing.hip -- to_affine + G2 line precomputation (mod.rs:199-216, 701-727) and the
+// Miller loop (mod.rs:579-607), one lane per pairing.
+#include "kernels.h"
+
+namespace bn {
+
+// ---------------------------------------------------------------- pairing kernels
+// flags[i]: 1 = skip (a zero point; pairing() returns Fq12::one(), mod.rs:896)
+// mode 1 (miller_loop_batch): a zero point sets *err = BN_ERR_TO_AFFINE (lib.rs:629-630)
+__global__ void __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
+                                                    uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff,
+                                                    uint8_t* __restrict__ flags, int* __restrict__ err, int mode) {
+    const size_t i = lane_id();
+    if (i >= n) return;
+    uint32_t w[8];
+    // to_affine (mod.rs:199-216); the z == 1 shortcut yields the same values as the general path
+    ld_words(&p[i].z, w);
+    const bool p_zero = words_zero(w);
+    const Fq<2> pz = fq_load_ref(w);
+    uint32_t w0[8], w1[8];
+    ld_words(&q[i].z.c0, w0);
+    ld_words(&q[i].z.c1, w1);
+    const bool q_zero = words_zero(w0) && words_zero(w1);
+    const Fq2<2> qz = {fq_load_ref(w0), fq_load_ref(w1)};
+    if ((p_zero || q_zero) && mode == 1) atomicOr(err, 1 << BN_ERR_TO_AFFINE);
+    flags[i] = (p_zero || q_zero) ? 1 : 0;
+
+    auto pzinv = fq_inv(pz);
+    auto pzinv2 = fq_sqr(pzinv);
+    auto px = fq_mul(ld_ref(p[i].x), pzinv2);
+    auto py = fq_mul(ld_ref(p[i].y), fq_mul(pzinv2, pzinv));
+    st_fq(paff, n, i, 0, px);
+    st_fq(paff, n, i, 1, py);
+
+    auto qzinv = fq2_inv(qz);
+    auto qzinv2 = fq2_sqr(qzinv);
+    G2Aff<kPt> qa = {narrow<kPt>(fq2_mul(ld_ref2(q[i].x), qzinv2)),
+                     narrow<kPt>(fq2_mul(ld_ref2(q[i].y), fq2_mul(qzinv2, qzinv)))};
+    g2_precompute(qa, [&](int k, const Ell& e) {
+        st_fq2(coeffs, n, i, k * 6 + 0, e.ell_0);
+        st_fq2(coeffs, n, i, k * 6 + 2, e.ell_vw);
+        st_fq2(coeffs, n, i, k * 6 + 4, e.ell_vv);
+    });
+}
+
+__global__ void __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ coeffs, const uint32_t* __restrict__ paff,
+                                                   const uint8_t* __restrict__ flags, size_t n, uint32_t* __restrict__ f_out) {
+    const size_t i = lane_id();
+    if (i >= n) return;
+    const Fq<2> px = ld_fq<2>(paff, n, i, 0);
+    const Fq<2> py = ld_fq<2>(paff, n, i, 1);
+    Fq12<kF> f = miller_loop(px, py, [&](int k) {
+        return Ell{ld_fq2<kLine>(coeffs, n, i, k * 6 + 0), ld_fq2<kLine>(coeffs, n, i, k * 6 + 2),
+                   ld_fq2<kLine>(coeffs, n, i, k * 6 + 4)};
+    });
+    if (flags[i]) f = widen<kF>(fq12_one());
+    st_fq12(f_out, n, i, f);
+}
+
+}  // namespace bn

@@ -1,0 +1,197 @@
+"""ctypes binding of libbn254mi.so (include/bn254mi.h).
+
+The product path: every call runs the HIP kernels on an MI355X.  There is no
+CPU fallback -- if the library or a GPU is missing the calls raise.
+Arrays are numpy uint64 in the reference memory image:
+  G1 (n, 12), G2 (n, 24), Gt (n, 48), Fr (n, 4).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libbn254mi.so")
+
+BN_OK = 0
+BN_ERR_INVALID_ARGUMENT = 1
+BN_ERR_TO_AFFINE = 2
+BN_ERR_FE_ZERO = 3
+BN_ERR_HIP = 4
+BN_ERR_NO_DEVICE = 5
+
+FQ12_OPS = {"mul": 0, "sqr": 1, "inv": 2, "cyc_sqr": 3, "exp_by_neg_z": 4, "frob1": 5, "frob2": 6, "frob3": 7}
+
+# every symbol include/bn254mi.h declares (checked by tests/test_capi_symbols.py)
+EXPORTS = [
+    "bn_ctx_create", "bn_ctx_destroy", "bn_last_error", "bn_ctx_stream",
+    "bn_pairing_many", "bn_pairing_many_dev", "bn_pairing_batch", "bn_miller_loop_batch",
+    "bn_final_exponentiation_many", "bn_miller_loop_many",
+    "bn_g1_mul_many", "bn_g1_mul_many_dev", "bn_g2_mul_many", "bn_g2_mul_many_dev",
+    "bn_fq12_op_many", "bn_workspace_bytes", "bn_reserve",
+]
+
+
+class BnError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("bn254mi error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def load():
+    """Load the native library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libbn254mi.so not built: run `make -C paritytech-bn_amd` "
+                          "(or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i, u8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p
+    sig = {
+        "bn_ctx_create": ([i, ctypes.POINTER(vp)], i),
+        "bn_ctx_destroy": ([vp], i),
+        "bn_last_error": ([vp], ctypes.c_char_p),
+        "bn_ctx_stream": ([vp], vp),
+        "bn_pairing_many": ([vp, vp, vp, sz, vp], i),
+        "bn_pairing_many_dev": ([vp, vp, vp, sz, vp, vp], i),
+        "bn_pairing_batch": ([vp, vp, vp, sz, vp], i),
+        "bn_miller_loop_batch": ([vp, vp, vp, sz, vp], i),
+        "bn_final_exponentiation_many": ([vp, vp, sz, vp, u8p], i),
+        "bn_miller_loop_many": ([vp, vp, vp, sz, vp], i),
+        "bn_g1_mul_many": ([vp, vp, vp, sz, vp], i),
+        "bn_g1_mul_many_dev": ([vp, vp, vp, sz, vp, vp], i),
+        "bn_g2_mul_many": ([vp, vp, vp, sz, vp], i),
+        "bn_g2_mul_many_dev": ([vp, vp, vp, sz, vp, vp], i),
+        "bn_fq12_op_many": ([vp, i, vp, vp, sz, vp], i),
+        "bn_workspace_bytes": ([sz], sz),
+        "bn_reserve": ([vp, sz], i),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _arr(a, width):
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    if a.size % width:
+        raise ValueError("array of %d words is not a multiple of %d" % (a.size, width))
+    return a.reshape(-1, width)
+
+
+class Context:
+    """One device context (bn_ctx).  All arrays are reference memory images."""
+
+    def __init__(self, device=0):
+        L = load()
+        h = ctypes.c_void_p()
+        rc = L.bn_ctx_create(device, ctypes.byref(h))
+        if rc != BN_OK:
+            raise BnError(rc, "bn_ctx_create(device=%d) failed" % device)
+        self._h = h
+        self._L = L
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.bn_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != BN_OK:
+            raise BnError(rc, (self._L.bn_last_error(self._h) or b"").decode())
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self):
+        return self._L.bn_ctx_stream(self._h)
+
+    # ---- pairing path
+    def pairing_many(self, p, q):
+        p, q = _arr(p, 12), _arr(q, 24)
+        if p.shape[0] != q.shape[0]:
+            raise ValueError("p and q lengths differ")
+        out = np.zeros((p.shape[0], 48), np.uint64)
+        self._check(self._L.bn_pairing_many(self._h, _ptr(p), _ptr(q), p.shape[0], _ptr(out)))
+        return out
+
+    def pairing_batch(self, p, q):
+        p, q = _arr(p, 12), _arr(q, 24)
+        out = np.zeros(48, np.uint64)
+        self._check(self._L.bn_pairing_batch(self._h, _ptr(p), _ptr(q), p.shape[0], _ptr(out)))
+        return out
+
+    def miller_loop_batch(self, q, p):
+        q, p = _arr(q, 24), _arr(p, 12)
+        out = np.zeros(48, np.uint64)
+        self._check(self._L.bn_miller_loop_batch(self._h, _ptr(q), _ptr(p), q.shape[0], _ptr(out)))
+        return out
+
+    def miller_loop_many(self, p, q):
+        p, q = _arr(p, 12), _arr(q, 24)
+        out = np.zeros((p.shape[0], 48), np.uint64)
+        self._check(self._L.bn_miller_loop_many(self._h, _ptr(p), _ptr(q), p.shape[0], _ptr(out)))
+        return out
+
+    def final_exponentiation_many(self, f):
+        f = _arr(f, 48)
+        out = np.zeros_like(f)
+        ok = np.zeros(f.shape[0], np.uint8)
+        self._check(self._L.bn_final_exponentiation_many(self._h, _ptr(f), f.shape[0], _ptr(out), _ptr(ok)))
+        return out, ok
+
+    # ---- group path
+    def g1_mul_many(self, p, k):
+        p, k = _arr(p, 12), _arr(k, 4)
+        out = np.zeros_like(p)
+        self._check(self._L.bn_g1_mul_many(self._h, _ptr(p), _ptr(k), p.shape[0], _ptr(out)))
+        return out
+
+    def g2_mul_many(self, p, k):
+        p, k = _arr(p, 24), _arr(k, 4)
+        out = np.zeros_like(p)
+        self._check(self._L.bn_g2_mul_many(self._h, _ptr(p), _ptr(k), p.shape[0], _ptr(out)))
+        return out
+
+    def fq12_op_many(self, op, a, b=None):
+        a = _arr(a, 48)
+        bb = _arr(b, 48) if b is not None else None
+        out = np.zeros_like(a)
+        self._check(self._L.bn_fq12_op_many(self._h, FQ12_OPS[op], _ptr(a), _ptr(bb) if bb is not None else None,
+                                            a.shape[0], _ptr(out)))
+        return out
+
+    # ---- device-pointer variants (ints: device addresses, e.g. torch tensor.data_ptr())
+    def pairing_many_dev(self, d_p, d_q, n, d_out, stream=None):
+        self._check(self._L.bn_pairing_many_dev(self._h, d_p, d_q, n, d_out, stream))
+
+    def g1_mul_many_dev(self, d_p, d_k, n, d_out, stream=None):
+        self._check(self._L.bn_g1_mul_many_dev(self._h, d_p, d_k, n, d_out, stream))
+
+    def g2_mul_many_dev(self, d_p, d_k, n, d_out, stream=None):
+        self._check(self._L.bn_g2_mul_many_dev(self._h, d_p, d_k, n, d_out, stream))
+
+    def reserve(self, n):
+        self._check(self._L.bn_reserve(self._h, n))
+
+
+def workspace_bytes(n):
+    return load().bn_workspace_bytes(n)

@@ -1,0 +1,170 @@
+"""Parity of the MI355X kernels (through the C ABI) with the CPU restatement
+oracle of substrate-bn 0.6.0, bit-exact, plus the reference's known answers.
+Runs on the GPU box: python -m pytest tests -m gpu."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+NT = 16  # oracle threads on the GPU box's host share
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from substrate_bn import Context
+    return Context(0)
+
+
+@pytest.fixture(scope="module")
+def pairs():
+    p, q, s, t = O.random_pairs(256, seed=1234, nthreads=NT)
+    return p, q
+
+
+def rnd_fq12(n, seed):
+    g = O.SplitMix64(seed)
+    return O.canon_to_mont_array([g.below(O.P) for _ in range(12 * n)]).reshape(n, 48)
+
+
+def test_fq12_ops(ctx):
+    a, b = rnd_fq12(64, 1), rnd_fq12(64, 2)
+    assert np.array_equal(ctx.fq12_op_many("mul", a, b), O.binary("orc_fq12_mul", a, b, 48, 48, 48))
+    assert np.array_equal(ctx.fq12_op_many("sqr", a), O.unary("orc_fq12_squared", a, 48)[0])
+    assert np.array_equal(ctx.fq12_op_many("inv", a), O.unary("orc_fq12_inverse", a, 48)[0])
+    assert np.array_equal(ctx.fq12_op_many("cyc_sqr", a), O.unary("orc_fq12_cyclotomic_squared", a, 48)[0])
+    assert np.array_equal(ctx.fq12_op_many("exp_by_neg_z", a[:16]), O.unary("orc_fq12_exp_by_neg_z", a[:16], 48)[0])
+    for pw in (1, 2, 3):
+        want = np.zeros_like(a)
+        for k in range(a.shape[0]):
+            O.lib().orc_fq12_frobenius_map(O._p(a[k]), pw, O._p(want[k]))
+        assert np.array_equal(ctx.fq12_op_many("frob%d" % pw, a), want)
+
+
+def test_cyclotomic_exp_kat(ctx, kats):
+    t = kats["test_cyclotomic_exp"]  # src/fields/mod.rs:230-344
+    got = ctx.fq12_op_many("exp_by_neg_z", O.canon_to_mont_array([int(x) for x in t["orig"]]))
+    assert O.mont_array_to_canon(got[0]) == [int(x) for x in t["expected"]]
+
+
+def test_g1_mul(ctx, pairs):
+    p, _ = pairs
+    ks, K = O.random_scalars(256, seed=77, lo=0)
+    assert np.array_equal(ctx.g1_mul_many(p, K), O.g1_mul(p, K, NT))
+    # edges: zero point, scalars 0, 1, r-1, 2^254-ish
+    z = np.zeros(12, np.uint64)
+    z[4:8] = O.canon_to_mont_array([1])
+    edge_p = np.stack([z, p[0], p[1], p[2], p[3]])
+    edge_k = O.canon_to_mont_array([5, 0, 1, O.R - 1, (1 << 253) + 12345], O.FR).reshape(5, 4)
+    assert np.array_equal(ctx.g1_mul_many(edge_p, edge_k), O.g1_mul(edge_p, edge_k))
+
+
+def test_g2_mul(ctx, pairs):
+    _, q = pairs
+    ks, K = O.random_scalars(64, seed=78)
+    assert np.array_equal(ctx.g2_mul_many(q[:64], K), O.g2_mul(q[:64], K, NT))
+
+
+def test_reference_kats(ctx, kats):
+    t = kats["test_reduced_pairing"]  # src/groups/mod.rs:929-999
+    p = O.g1_mul(O.g1_one(), O.canon_to_mont_array([int(t["g1_scalar"])], O.FR))
+    q = O.g2_mul(O.g2_one(), O.canon_to_mont_array([int(t["g2_scalar"])], O.FR))
+    gt = ctx.pairing_many(p, q)
+    assert O.mont_array_to_canon(gt[0]) == [int(x) for x in t["gt"]]
+    m = kats["test_miller_loop"]  # src/groups/mod.rs:643-691
+    f = ctx.miller_loop_many(p, q)
+    assert O.mont_array_to_canon(f[0]) == [int(x) for x in m["f"]]
+    f2 = ctx.miller_loop_batch(q, p)
+    assert np.array_equal(f2, f[0])
+
+
+def test_config1(ctx):
+    """e(G1::one(), G2::one()) == oracle (BASELINE config 1)."""
+    assert np.array_equal(ctx.pairing_many(O.g1_one(), O.g2_one()), O.pairing_many(O.g1_one(), O.g2_one()))
+
+
+def test_pairing_many(ctx, pairs):
+    p, q = pairs
+    assert np.array_equal(ctx.pairing_many(p, q), O.pairing_many(p, q, NT))
+
+
+def test_miller_and_final_exp(ctx, pairs):
+    p, q = pairs
+    f = ctx.miller_loop_many(p[:64], q[:64])
+    want_f = np.stack([O.miller_loop_batch(q[k], p[k])[1] for k in range(64)])
+    assert np.array_equal(f, want_f)
+    fe, ok = ctx.final_exponentiation_many(f)
+    assert ok.all() and np.array_equal(fe, O.pairing_many(p[:64], q[:64], NT))
+    # f == 0 -> None (fq12.rs:63-72)
+    fe0, ok0 = ctx.final_exponentiation_many(np.zeros((2, 48), np.uint64))
+    assert not ok0.any() and not fe0.any()
+
+
+def test_zero_points(ctx, pairs):
+    """pairing() of a zero point is Fq12::one() (mod.rs:896)."""
+    p, q = pairs
+    p2, q2 = p[:4].copy(), q[:4].copy()
+    one = O.canon_to_mont_array([1])
+    p2[1] = 0
+    p2[1, 4:8] = one                 # G1::zero()
+    q2[2] = 0
+    q2[2, 8:12] = one                # G2::zero(): y = (1, 0)
+    assert np.array_equal(ctx.pairing_many(p2, q2), O.pairing_many(p2, q2))
+
+
+@pytest.mark.parametrize("n", [0, 1, 5, 64])
+def test_pairing_batch(ctx, pairs, n):
+    p, q = pairs
+    p2, q2 = p[:n].copy(), q[:n].copy()
+    if n >= 5:
+        p2[3] = 0
+        p2[3, 4:8] = O.canon_to_mont_array([1])   # skipped pair
+    assert np.array_equal(ctx.pairing_batch(p2, q2), O.pairing_batch(p2, q2))
+
+
+def test_miller_loop_batch(ctx, pairs):
+    from substrate_bn import BnError
+    p, q = pairs
+    rc, want = O.miller_loop_batch(q[:33], p[:33])
+    assert rc == 0 and np.array_equal(ctx.miller_loop_batch(q[:33], p[:33]), want)
+    p2 = p[:3].copy()
+    p2[1] = 0
+    with pytest.raises(BnError):
+        ctx.miller_loop_batch(q[:3], p2)
+
+
+def test_rust_api_mirror(ctx):
+    """The substrate_bn mirror reads like the reference's own tests."""
+    import substrate_bn as bn
+    s = bn.Fr.from_int(0x1234567)
+    a = bn.pairing(bn.G1.one() * s, bn.G2.one())
+    b = bn.pairing(bn.G1.one(), bn.G2.one() * s)
+    assert a == b and a != bn.Gt.one()
+    assert bn.pairing(bn.G1.zero(), bn.G2.one()) == bn.Gt.one()
+    assert bn.pairing_batch([]) == bn.Gt.one()
+    with pytest.raises(bn.CurveError):
+        bn.miller_loop_batch([(bn.G2.one(), bn.G1.zero())])
+    assert bn.miller_loop_batch([(bn.G2.one(), bn.G1.one())]).final_exponentiation() == \
+        bn.pairing(bn.G1.one(), bn.G2.one())
+
+
+def test_large_batch_parity_and_bilinearity(ctx):
+    """4096 pairings bit-exact vs the oracle, then the size-independent checks at
+    2^16 (BASELINE config 2): bilinearity e(sP, Q) == e(P, sQ) on every lane."""
+    p, q, _, _ = O.random_pairs(4096, seed=4096, nthreads=NT)
+    got = ctx.pairing_many(p, q)
+    assert np.array_equal(got, O.pairing_many(p, q, NT))
+    n = 1 << 16
+    s_vals, S = O.random_scalars(n, seed=7)
+    base1 = np.tile(O.g1_one(), (n, 1))
+    base2 = np.tile(O.g2_one(), (n, 1))
+    P = ctx.g1_mul_many(base1, S)
+    Q = ctx.g2_mul_many(base2, np.roll(S, 1, axis=0))
+    sP = ctx.g1_mul_many(P, np.roll(S, 2, axis=0))
+    sQ = ctx.g2_mul_many(Q, np.roll(S, 2, axis=0))
+    e1 = ctx.pairing_many(sP, Q)
+    e2 = ctx.pairing_many(P, sQ)
+    assert np.array_equal(e1, e2)
+    # spot-check a sample of lanes against the oracle
+    idx = np.random.default_rng(0).choice(n, 256, replace=False)
+    assert np.array_equal(e1[idx], O.pairing_many(sP[idx], Q[idx], NT))
