@@ -98,6 +98,15 @@ typedef enum {
 } bn_fq12_op;
 int bn_fq12_op_many(bn_ctx* ctx, int op, const bn_gt* a, const bn_gt* b, size_t n, bn_gt* out);
 
+/* ---- measurement ---- */
+/* enable HIP-event timing of each kernel phase of bn_pairing_many_dev (events are
+ * recorded on the launch stream between the kernels) */
+int bn_set_phase_timing(bn_ctx* ctx, int enable);
+/* device milliseconds per phase since the last read: ms[0] k_prepare (to_affine +
+ * G2 lines), ms[1] k_miller, ms[2] k_fq12_vm (final exponentiation), ms[3] k_fe_out;
+ * *launches = launch sets measured */
+int bn_get_phase_times(bn_ctx* ctx, float ms[4], int* launches);
+
 /* ---- workspace ---- */
 /* device bytes the context holds for a batch of n pairings (allocated on first use) */
 size_t bn_workspace_bytes(size_t n);

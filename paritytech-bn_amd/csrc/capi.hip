@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <array>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -24,6 +25,10 @@ struct bn_ctx {
     uint32_t* slots = nullptr;  // Fq12 slots of the step machine; slot 0 = Miller values
     uint8_t* flags = nullptr;
     uint32_t* d_prog = nullptr; // final-exponentiation step program
+    // optional per-phase timing of bn_pairing_many_dev (HIP events on the launch stream)
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::array<hipEvent_t, 5>> ev_marks;
     int fe_steps = 0;
     int fe_out = 0;
     int* d_err = nullptr;
@@ -241,6 +246,10 @@ int bn_ctx_destroy(bn_ctx* c) {
     for (void* p : {(void*)c->coeffs, (void*)c->paff, (void*)c->slots, (void*)c->flags, (void*)c->d_err,
                     (void*)c->d_prog, c->stage})
         if (p) hipFree(p);
+    for (auto& ev : c->ev_marks)
+        for (auto e : ev) c->ev_pool.push_back(e);
+    for (auto e : c->ev_pool)
+        if (e) hipEventDestroy(e);
     hipStreamDestroy(c->stream);
     delete c;
     return BN_OK;
@@ -255,6 +264,17 @@ int bn_reserve(bn_ctx* c, size_t n) {
     return reserve(c, n < kChunk ? n : kChunk);
 }
 
+static hipEvent_t take_event(bn_ctx* c) {
+    if (c->ev_pool.empty()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        return e;
+    }
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+}
+
 int bn_pairing_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, void* stream) {
     CTX_GUARD(c);
     if (n == 0) return BN_OK;
@@ -263,9 +283,52 @@ int bn_pairing_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n,
     RET_IF(reserve(c, n < kChunk ? n : kChunk));
     for (size_t off = 0; off < n; off += kChunk) {
         const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
-        RET_IF(miller_values(c, d_p + off, d_q + off, m, 0, s));
-        RET_IF(run_fe(c, m, c->flags, d_out + off, nullptr, s));
+        std::array<hipEvent_t, 5> ev{};
+        if (c->timing)
+            for (auto& e : ev) e = take_event(c);
+        auto mark = [&](int k) {
+            if (c->timing && ev[k]) hipEventRecord(ev[k], s);
+        };
+        mark(0);
+        k_prepare<<<grid_for(m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags, c->d_err, 0);
+        mark(1);
+        k_miller<<<grid_for(m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, c->slots);
+        mark(2);
+        k_fq12_vm<<<grid_for(m), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, m);
+        mark(3);
+        k_fe_out<<<grid_for(m), kBlock, 0, s>>>(c->slots, m, c->fe_out, c->flags, d_out + off, nullptr, c->d_err);
+        mark(4);
+        HIPCHK(c, hipGetLastError());
+        if (c->timing) c->ev_marks.push_back(ev);
     }
+    return BN_OK;
+}
+
+int bn_set_phase_timing(bn_ctx* c, int enable) {
+    CTX_GUARD(c);
+    c->timing = enable != 0;
+    return BN_OK;
+}
+
+// per-phase device time of the bn_pairing_many_dev calls since the last read:
+// ms[0..3] = k_prepare, k_miller, k_fq12_vm (final exponentiation), k_fe_out;
+// *launches = chunk launch sets measured.  Synchronizes on the recorded events.
+int bn_get_phase_times(bn_ctx* c, float* ms, int* launches) {
+    CTX_GUARD(c);
+    if (!ms || !launches) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    for (int k = 0; k < 4; ++k) ms[k] = 0.f;
+    *launches = 0;
+    for (auto& ev : c->ev_marks) {
+        HIPCHK(c, hipEventSynchronize(ev[4]));
+        for (int k = 0; k < 4; ++k) {
+            float t = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&t, ev[k], ev[k + 1]));
+            ms[k] += t;
+        }
+        ++*launches;
+        for (auto e : ev) c->ev_pool.push_back(e);
+    }
+    c->ev_marks.clear();
     return BN_OK;
 }
 

@@ -28,7 +28,7 @@ EXPORTS = [
     "bn_pairing_many", "bn_pairing_many_dev", "bn_pairing_batch", "bn_miller_loop_batch",
     "bn_final_exponentiation_many", "bn_miller_loop_many",
     "bn_g1_mul_many", "bn_g1_mul_many_dev", "bn_g2_mul_many", "bn_g2_mul_many_dev",
-    "bn_fq12_op_many", "bn_workspace_bytes", "bn_reserve",
+    "bn_fq12_op_many", "bn_workspace_bytes", "bn_reserve", "bn_set_phase_timing", "bn_get_phase_times",
 ]
 
 
@@ -69,6 +69,8 @@ def load():
         "bn_fq12_op_many": ([vp, i, vp, vp, sz, vp], i),
         "bn_workspace_bytes": ([sz], sz),
         "bn_reserve": ([vp, sz], i),
+        "bn_set_phase_timing": ([vp, i], i),
+        "bn_get_phase_times": ([vp, vp, vp], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -188,6 +190,16 @@ class Context:
 
     def g2_mul_many_dev(self, d_p, d_k, n, d_out, stream=None):
         self._check(self._L.bn_g2_mul_many_dev(self._h, d_p, d_k, n, d_out, stream))
+
+    def set_phase_timing(self, enable=True):
+        self._check(self._L.bn_set_phase_timing(self._h, 1 if enable else 0))
+
+    def phase_times(self):
+        """(ms per phase [prepare, miller, final_exp, fe_out], launch sets) since the last read."""
+        ms = np.zeros(4, np.float32)
+        cnt = np.zeros(1, np.int32)
+        self._check(self._L.bn_get_phase_times(self._h, _ptr(ms), _ptr(cnt)))
+        return ms.astype(float), int(cnt[0])
 
     def reserve(self, n):
         self._check(self._L.bn_reserve(self._h, n))
