@@ -62,7 +62,9 @@ struct Prog {
     uint32_t next = 2;
     uint32_t tmp() { return next++; }
     void op(Fq12Op o, uint32_t d, uint32_t a, uint32_t b = 0) { s.push_back(vm_step(o, d, a, b)); }
-    // exp_by_neg_z, fq12.rs:121-124 + cyclotomic_pow fq12.rs:249-266 (u = 0x44e992b44a6909f1)
+    // exp_by_neg_z, fq12.rs:121-124 + cyclotomic_pow fq12.rs:249-266 (u = 0x44e992b44a6909f1).
+    // (A register-resident OP_EXPZ spills ~900 VGPRs: base + accumulator + product temporaries
+    // exceed 512, so the loop runs as steps; see DESIGN.md.)
     uint32_t exp_by_neg_z(uint32_t x) {
         const uint64_t u = 4965661367192848881ull;
         const uint32_t r = tmp();

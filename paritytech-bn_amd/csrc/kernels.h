@@ -8,7 +8,10 @@
 
 namespace bn {
 
-constexpr int kBlock = 64;               // one wave per workgroup: even spread over SIMDs
+// 256 threads = 4 waves: the dispatcher puts one such workgroup per CU, one wave
+// per SIMD (measured census, profiles/r1_ubench3.jsonl); 64-thread workgroups
+// left 104 of 1024 SIMDs with two waves while others idled.
+constexpr int kBlock = 256;
 constexpr int kCoeffFq = BN_NUM_COEFFS * 6;  // Fq elements of line coefficients per pairing
 constexpr size_t kChunk = size_t(1) << 18;   // pairings per launch set (~5 GB workspace)
 
