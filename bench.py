@@ -77,6 +77,63 @@ def pmc_traffic(kernel):
         return None
 
 
+def other_workload(args, local_rank):
+    """BASELINE config 3 (batched G1 * Fr) and config 5 (pairing product), 1 GPU."""
+    import torch
+
+    from oracle import oracle as O
+    from substrate_bn import Context
+
+    dev = torch.device("cuda", local_rank)
+    ctx = Context(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    res = {"n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)", "data": "synthetic"}
+    if args.workload == "g1mul":
+        n = args.pairs if args.pairs != (1 << 16) else (1 << 18)
+        base = torch.from_numpy(np.tile(O.g1_one().view(np.int64), (n, 1))).to(dev)
+        k1 = torch.from_numpy(fr_images(n, 5).view(np.int64)).to(dev)
+        k2 = torch.from_numpy(fr_images(n, 6).view(np.int64)).to(dev)
+        P = torch.empty((n, 12), dtype=torch.int64, device=dev)
+        out = torch.empty_like(P)
+        ctx.g1_mul_many_dev(base.data_ptr(), k1.data_ptr(), n, P.data_ptr(), sh)  # random Jacobian bases
+        step = lambda: ctx.g1_mul_many_dev(P.data_ptr(), k2.data_ptr(), n, out.data_ptr(), sh)  # noqa: E731
+        unit = "G1 scalar muls/s"
+        res["config"] = {"workload": "BASELINE config 3: batched Fr x G1 (reference double-and-add chain, "
+                                     "bit-exact Jacobian output)", "muls": n}
+    else:
+        n = args.pairs if args.pairs != (1 << 16) else (1 << 14)
+        p, q, _, _ = O.random_pairs(n, seed=21, nthreads=min(16, os.cpu_count() or 1))
+        step = lambda: ctx.pairing_batch(p, q)  # noqa: E731
+        unit = "pairing-product terms/s"
+        res["config"] = {"workload": "BASELINE config 5: one pairing_batch over 2^14 terms (per-term Miller "
+                                     "values, product tree, one final exponentiation; host buffers incl. PCIe)",
+                         "terms": n}
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    res.update({"metric": unit, "value": n * args.steps / el, "unit": unit, "ms_per_step": el / args.steps * 1e3})
+    if args.workload == "g1mul":
+        m = min(args.cpu_sample, n)
+        threads = min(16, os.cpu_count() or 1)
+        ph, kh, oh = (t[:m].cpu().numpy().view(np.uint64) for t in (P, k2, out))
+        t0 = time.perf_counter()
+        ref = O.g1_mul(ph, kh, threads)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": m / dt, "unit": unit, "cores": threads, "kind": "port",
+                               "sample": "%d G1*Fr of the bench inputs, oracle, %d threads" % (m, threads),
+                               "parity_sample_bit_exact": bool(np.array_equal(ref, oh))}
+    else:
+        res["parity_bit_exact"] = bool(np.array_equal(ctx.pairing_batch(p, q), O.pairing_batch(p[:n], q[:n])))
+    print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +142,9 @@ def main():
     ap.add_argument("--pairs", type=int, default=1 << 16, help="pairings per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="pairing", choices=["pairing", "g1mul", "product"],
+                    help="pairing: config 2 (default); g1mul: config 3 (2^18 G1*Fr); product: config 5 "
+                         "(2^14-term pairing_batch)")
     args = ap.parse_args()
 
     import torch
@@ -103,6 +163,9 @@ def main():
 
     from substrate_bn import Context
     from oracle import oracle as O
+
+    if args.workload != "pairing":
+        return other_workload(args, local_rank)
 
     n = args.pairs
     ctx = Context(local_rank)
