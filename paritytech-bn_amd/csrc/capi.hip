@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <array>
 #include <mutex>
 #include <string>
@@ -58,60 +59,88 @@ size_t ws_bytes(size_t n) {
 
 // ---------------------------------------------------------------- FE step program
 struct Prog {
-    std::vector<uint32_t> s;
+    std::vector<uint32_t> s;  // two words per step (kernels.h)
     uint32_t next = 2;
     uint32_t tmp() { return next++; }
-    void op(Fq12Op o, uint32_t d, uint32_t a, uint32_t b = 0) { s.push_back(vm_step(o, d, a, b)); }
-    // exp_by_neg_z, fq12.rs:121-124 + cyclotomic_pow fq12.rs:249-266 (u = 0x44e992b44a6909f1).
-    // (A register-resident OP_EXPZ spills ~900 VGPRs: base + accumulator + product temporaries
-    // exceed 512, so the loop runs as steps; see DESIGN.md.)
-    uint32_t exp_by_neg_z(uint32_t x) {
-        const uint64_t u = 4965661367192848881ull;
+    int steps() const { return (int)(s.size() / 2); }
+    void op(Fq12Op o, uint32_t d, uint32_t a, uint32_t b = 0, uint32_t k = 0, uint32_t flags = 0) {
+        uint32_t w[2];
+        vm_step(w, o, d, a, b, o == OP_CYC && k == 0 ? 1 : k, flags);
+        s.push_back(w[0]);
+        s.push_back(w[1]);
+    }
+    // x^e for a signed-digit chain (digit, position) from the top digit (+1)
+    // down, each run "square k times, multiply by x or conj(x)" as one step;
+    // the last step conjugates when `conj_out`.
+    uint32_t chain(uint32_t x, const std::vector<std::pair<int, int>>& digits, bool conj_out) {
         const uint32_t r = tmp();
-        op(OP_MOV, r, x);  // first set bit (62): one * x
-        for (int bit = 61; bit >= 0; --bit) {
-            op(OP_CYC, r, r);
-            if ((u >> bit) & 1) op(OP_MUL, r, x, r);
+        int pos = digits[0].second;
+        uint32_t src = x;
+        for (size_t t = 1; t < digits.size(); ++t) {
+            const bool last = t + 1 == digits.size() && digits[t].second == 0;
+            op(OP_MUL, r, src, x, (uint32_t)(pos - digits[t].second),
+               (digits[t].first < 0 ? kFlagConjB : 0) | (last && conj_out ? kFlagConjOut : 0));
+            pos = digits[t].second;
+            src = r;
         }
-        op(OP_CONJ, r, r);
+        if (pos > 0) {
+            op(OP_CYC, r, src, 0, (uint32_t)pos);
+            if (conj_out) op(OP_CONJ, r, r);
+        } else if (src == x) {  // a single digit at position 0: x itself
+            op(conj_out ? OP_CONJ : OP_MOV, r, x);
+        }
         return r;
     }
+    // exp_by_neg_z, fq12.rs:121-124: conj(cyclotomic_pow(u)) with
+    // u = 0x44e992b44a6909f1 (fq12.rs:249-266).  `naf` = use the 24-digit
+    // signed form of u, valid when x is in the cyclotomic subgroup (there
+    // conj(x) = x^-1) -- always true inside the final exponentiation; the
+    // generic op (bn_fq12_op_many) keeps the reference's binary chain so its
+    // output matches the reference for any input.
+    uint32_t exp_by_neg_z(uint32_t x, bool naf = false) {
+        uint64_t u = 4965661367192848881ull;
+        std::vector<std::pair<int, int>> d;  // (digit, position), low to high
+        for (int pos = 0; u; ++pos, u >>= 1) {
+            if (!(u & 1)) continue;
+            int z = 1;
+            if (naf && (u & 3) == 3) z = -1;
+            d.push_back({z, pos});
+            u -= (uint64_t)(int64_t)z;  // u - z is even
+        }
+        std::reverse(d.begin(), d.end());
+        return chain(x, d, true);
+    }
 };
-// final_exponentiation (fq12.rs:107-110) of slot 0; returns the result slot
+// final_exponentiation (fq12.rs:107-110) of slot 0; returns the result slot.
+// Same operations as the reference; conjugations ride on the multiplies.
 uint32_t build_final_exp(Prog& P) {
     // first chunk, fq12.rs:62-73
-    const uint32_t b = P.tmp(), a = P.tmp(), c = P.tmp(), d = P.tmp();
+    const uint32_t b = P.tmp(), c = P.tmp(), d = P.tmp();
     P.op(OP_INV, b, 0);
-    P.op(OP_CONJ, a, 0);
-    P.op(OP_MUL, c, a, b);
+    P.op(OP_MUL, c, b, 0, 0, kFlagConjB);  // c = conj(f) * f^-1
     P.op(OP_FROB2, d, c);
     P.op(OP_MUL, 1, d, c);  // slot 1 = self of the last chunk
     // last chunk, fq12.rs:75-105
-    const uint32_t A = P.exp_by_neg_z(1);
-    const uint32_t B = P.tmp(), C = P.tmp(), D = P.tmp();
-    P.op(OP_CYC, B, A);
-    P.op(OP_CYC, C, B);
-    P.op(OP_MUL, D, C, B);
-    const uint32_t E = P.exp_by_neg_z(D);
+    const uint32_t A = P.exp_by_neg_z(1, true);
+    const uint32_t B = P.tmp(), D = P.tmp();
+    P.op(OP_CYC, B, A, 0, 1);
+    P.op(OP_MUL, D, B, B, 1);  // d = cyc(b) * b
+    const uint32_t E = P.exp_by_neg_z(D, true);
     const uint32_t F = P.tmp();
-    P.op(OP_CYC, F, E);
-    const uint32_t G = P.exp_by_neg_z(F);
-    const uint32_t H = P.tmp(), I = P.tmp(), J = P.tmp(), K = P.tmp(), L = P.tmp(), M = P.tmp(), N = P.tmp();
-    P.op(OP_CONJ, H, D);
-    P.op(OP_CONJ, I, G);
-    P.op(OP_MUL, J, I, E);
-    P.op(OP_MUL, K, J, H);
+    P.op(OP_CYC, F, E, 0, 1);
+    const uint32_t G = P.exp_by_neg_z(F, true);
+    const uint32_t J = P.tmp(), K = P.tmp(), L = P.tmp(), M = P.tmp(), N = P.tmp();
+    P.op(OP_MUL, J, E, G, 0, kFlagConjB);  // j = conj(g) * e
+    P.op(OP_MUL, K, J, D, 0, kFlagConjB);  // k = j * conj(d)
     P.op(OP_MUL, L, K, B);
     P.op(OP_MUL, M, K, E);
     P.op(OP_MUL, N, 1, M);
-    const uint32_t O = P.tmp(), Pp = P.tmp(), Q = P.tmp(), R = P.tmp(), S = P.tmp(), T = P.tmp(), U = P.tmp(),
-                   V = P.tmp();
+    const uint32_t O = P.tmp(), Pp = P.tmp(), Q = P.tmp(), R = P.tmp(), T = P.tmp(), U = P.tmp(), V = P.tmp();
     P.op(OP_FROB1, O, L);
     P.op(OP_MUL, Pp, O, N);
     P.op(OP_FROB2, Q, K);
     P.op(OP_MUL, R, Q, Pp);
-    P.op(OP_CONJ, S, 1);
-    P.op(OP_MUL, T, S, L);
+    P.op(OP_MUL, T, L, 1, 0, kFlagConjB);  // t = conj(self) * l
     P.op(OP_FROB3, U, T);
     P.op(OP_MUL, V, U, R);
     return V;
@@ -225,7 +254,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
     c->device = device;
     Prog P;
     c->fe_out = (int)build_final_exp(P);
-    c->fe_steps = (int)P.s.size();
+    c->fe_steps = P.steps();
     if (P.next > (uint32_t)kFeSlots) {
         delete c;
         return BN_ERR_INVALID_ARGUMENT;
@@ -548,7 +577,7 @@ int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n,
             default: P.op(OP_FROB3, res, 1); break;
         }
         HIPCHK(c, hipMemcpyAsync(dprog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice, c->stream));
-        k_fq12_vm<<<grid_for(m), kBlock, 0, c->stream>>>(dprog, (int)P.s.size(), c->slots, m);
+        k_fq12_vm<<<grid_for(m), kBlock, 0, c->stream>>>(dprog, P.steps(), c->slots, m);
         k_gt_store<<<grid_for(m), kBlock, 0, c->stream>>>(c->slots + (size_t)res * kSlotWords * m, m, m, dout);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));

@@ -150,15 +150,21 @@ inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 // enormous kernel (minutes to build, scratch spills).  Instead k_fq12_vm runs a
 // step program over lane-strided Fq12 slots in HBM: each step loads its
 // operands, computes in registers, stores the result.  Every operation's code
-// exists once; the operand traffic (<= 1.3 KB per lane per Fq12 product, which
-// itself takes ~50k cycles) is negligible.  The opcode is wave-uniform.
+// exists once.  The opcode is wave-uniform.  A step is two words:
+//   w0 = op | d << 8 | a << 16 | b << 24,   w1 = k | flags << 8
+// OP_CYC:  d = cyc^k(a)                       (k cyclotomic squarings in registers)
+// OP_MUL:  d = [conj] (cyc^k(a) * [conj] b)   (kFlagConjB, kFlagConjOut)
+// so a whole run of an exponent chain (zeros then a digit) is one step and the
+// slot traffic is paid once per nonzero digit, not once per squaring.
 enum Fq12Op : uint32_t {
     OP_MOV = 0, OP_MUL = 1, OP_SQR = 2, OP_CYC = 3, OP_CONJ = 4,
     OP_FROB1 = 5, OP_FROB2 = 6, OP_FROB3 = 7, OP_INV = 8
 };
+constexpr uint32_t kFlagConjB = 1, kFlagConjOut = 2;
 constexpr int kSlotWords = 108;  // 12 Fq x 9 digits
-inline uint32_t vm_step(uint32_t op, uint32_t d, uint32_t a, uint32_t b = 0) {
-    return op | (d << 8) | (a << 16) | (b << 24);
+inline void vm_step(uint32_t out[2], uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t k, uint32_t flags) {
+    out[0] = op | (d << 8) | (a << 16) | (b << 24);
+    out[1] = k | (flags << 8);
 }
 
 // ---------------------------------------------------------------- kernels

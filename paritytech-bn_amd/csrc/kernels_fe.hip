@@ -14,16 +14,33 @@ __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__
     if (i >= n) return;
 #pragma unroll 1
     for (int pc = 0; pc < nsteps; ++pc) {
-        const uint32_t ins = prog[pc];  // uniform: scalar load
-        const uint32_t op = ins & 0xff;
+        const uint32_t ins = prog[2 * pc];  // uniform: scalar loads
+        const uint32_t aux = prog[2 * pc + 1];
+        const uint32_t op = ins & 0xff, k = aux & 0xff, flags = aux >> 8;
         uint32_t* d = slot_ptr(slots, n, (ins >> 8) & 0xff);
         const uint32_t* a = slot_ptr(slots, n, (ins >> 16) & 0xff);
         const uint32_t* b = slot_ptr(slots, n, ins >> 24);
         switch (op) {
             case OP_MOV: st_fq12(d, n, i, ld_fq12<kF>(a, n, i)); break;
-            case OP_MUL: st_fq12(d, n, i, mul12(ld_fq12<kF>(a, n, i), ld_fq12<kF>(b, n, i))); break;
+            case OP_MUL: {
+                Fq12<kF> x = ld_fq12<kF>(a, n, i);
+#pragma unroll 1
+                for (uint32_t j = 0; j < k; ++j) x = cyc_sqr(x);
+                Fq12<kF> y = ld_fq12<kF>(b, n, i);
+                if (flags & kFlagConjB) y = fq12_conj(y);
+                Fq12<kF> r = mul12(x, y);
+                if (flags & kFlagConjOut) r = fq12_conj(r);
+                st_fq12(d, n, i, r);
+                break;
+            }
             case OP_SQR: st_fq12(d, n, i, narrow12<kF>(fq12_sqr(ld_fq12<kF>(a, n, i)))); break;
-            case OP_CYC: st_fq12(d, n, i, cyc_sqr(ld_fq12<kF>(a, n, i))); break;
+            case OP_CYC: {
+                Fq12<kF> x = ld_fq12<kF>(a, n, i);
+#pragma unroll 1
+                for (uint32_t j = 0; j < k; ++j) x = cyc_sqr(x);
+                st_fq12(d, n, i, x);
+                break;
+            }
             case OP_CONJ: st_fq12(d, n, i, fq12_conj(ld_fq12<kF>(a, n, i))); break;
             case OP_FROB1: st_fq12(d, n, i, narrow12<kF>(fq12_frobenius_map<1>(ld_fq12<kF>(a, n, i)))); break;
             case OP_FROB2: st_fq12(d, n, i, narrow12<kF>(fq12_frobenius_map<2>(ld_fq12<kF>(a, n, i)))); break;
