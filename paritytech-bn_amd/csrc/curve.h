@@ -41,6 +41,10 @@ BN_INLINE auto F_neg(const Fq2<A>& a) { return fq2_neg(a); }
 template <int A>
 BN_INLINE auto F_fold(const Fq<A>& a) { return fq_fold(a); }
 template <int A>
+BN_INLINE auto F_norm(const Fq<A>& a) { return fq_norm(a); }
+template <int A>
+BN_INLINE auto F_norm(const Fq2<A>& a) { return fq2_norm(a); }
+template <int A>
 BN_INLINE auto F_fold(const Fq2<A>& a) { return fq2_fold(a); }
 template <int A>
 BN_INLINE bool F_is_zero(const Fq<A>& a) { return fq_is_zero(a); }
@@ -63,8 +67,8 @@ BN_INLINE Fq2<B> F_select(bool c, const Fq2<B>& a, const Fq2<B>& b) { return fq2
 template <int S, template <int> class F, int B>
 BN_INLINE F<S> narrow(const F<B>& a) {
     static_assert(S >= 2, "storage bound must admit a folded value");
-    if constexpr (B <= S) {
-        return F_widen<S>(a);
+    if constexpr (kv(B) <= S) {
+        return F_widen<S>(F_norm(a));
     } else {
         return F_widen<S>(F_fold(a));
     }

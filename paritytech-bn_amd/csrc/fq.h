@@ -33,6 +33,10 @@
 #define BN_INLINE inline __attribute__((always_inline))
 #endif
 
+#ifndef BN_FENCE_FQ
+#define BN_FENCE_FQ 0
+#endif
+
 namespace bn {
 
 #include "constants.inc"
@@ -43,26 +47,58 @@ struct Limbs9 {
 };
 constexpr Limbs9 kP29 = {BN_P29};
 
-// value bound bookkeeping ------------------------------------------------
+// bound bookkeeping ------------------------------------------------------
+// An Fq carries a compile-time bound code K = B + 256*(L-1):
+//   B = value bound: value <= B*p (B <= 160, so value < 2^261);
+//   L = digit bound: every digit < L*2^29 (L == 1: normalized).
+// Additions, subtractions and small multiples leave digits unnormalized
+// ("lazy", one VOP2 per digit) while L stays <= kMaxLimb; a Montgomery product
+// accepts La*Lb <= 6 (its column sums stay below 2^64) and normalizes an
+// operand first otherwise.  Normalized values have K == B, so plain bounds read
+// as before.
 // p / 2^261 < 0.005908 ; output of a Montgomery product of values <= A*p, <= B*p
 // is <= (1 + A*B*p/R) * p.
 constexpr int mul_bound(int A, int B) { return 1 + (int)(((long long)A * B * 5908 + 999999) / 1000000); }
 constexpr int kMaxBound = 160;  // 160 * p < 2^261
+constexpr int kMaxLimb = 7;     // digits < 7*2^29: a carry pass cannot overflow 32 bits
+constexpr int kv(int K) { return K & 255; }
+constexpr int kl(int K) { return (K >> 8) + 1; }
+constexpr int kenc(int B, int L) { return B + 256 * (L - 1); }
+constexpr int kjoin(int A, int B) {
+    return kenc(kv(A) > kv(B) ? kv(A) : kv(B), kl(A) > kl(B) ? kl(A) : kl(B));
+}
 
-template <int B>
+template <int K>
 struct Fq {
-    static_assert(B >= 1 && B <= kMaxBound, "Fq value bound out of range");
+    static_assert(kv(K) >= 1 && kv(K) <= kMaxBound, "Fq value bound out of range");
+    static_assert(kl(K) >= 1 && kl(K) <= kMaxLimb, "Fq digit bound out of range");
     uint32_t v[9];
 };
 
 // widen the static bound (free)
-template <int B2, int B>
-BN_INLINE Fq<B2> widen(const Fq<B>& a) {
-    static_assert(B <= B2, "widen: narrowing");
-    Fq<B2> r;
+template <int K2, int K>
+BN_INLINE Fq<K2> widen(const Fq<K>& a) {
+    static_assert(kv(K) <= kv(K2) && kl(K) <= kl(K2), "widen: narrowing");
+    Fq<K2> r;
 #pragma unroll
     for (int i = 0; i < 9; ++i) r.v[i] = a.v[i];
     return r;
+}
+
+// Register fence: the digits pass through an empty volatile asm.  Work that
+// consumes a fenced value cannot start before the fence and volatile asms keep
+// program order, so fencing a product's inputs and its result serializes the
+// products in program order.  This bounds the compiler's interleaving of
+// independent products (which otherwise keeps dozens of partial products live
+// and spills); it emits no instruction.
+template <int B>
+BN_INLINE void fq_fence(Fq<B>& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(a.v[0]), "+v"(a.v[1]), "+v"(a.v[2]), "+v"(a.v[3]), "+v"(a.v[4]), "+v"(a.v[5]),
+                 "+v"(a.v[6]), "+v"(a.v[7]), "+v"(a.v[8]));
+#else
+    (void)a;
+#endif
 }
 
 template <int B = 1>
@@ -75,32 +111,44 @@ BN_INLINE Fq<B> fq_from_limbs(const Limbs9& l) {
 BN_INLINE Fq<1> fq_zero() { return fq_from_limbs<1>(Limbs9{{0, 0, 0, 0, 0, 0, 0, 0, 0}}); }
 BN_INLINE Fq<1> fq_one() { return fq_from_limbs<1>(Limbs9{BN_ONE}); }
 
-// carry-propagate digits 0..7 into 8 (full-rate VOP2: lshr, and, add)
-template <int B>
-BN_INLINE void fq_normalize(Fq<B>& r) {
+// carry-propagate digits 0..7 into 8 (full-rate VOP2: lshr, and, add); the
+// top digit stays < 2^29 because the value is < 2^261
+template <int K>
+BN_INLINE Fq<kv(K)> fq_norm(const Fq<K>& a) {
+    Fq<kv(K)> r;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        r.v[i + 1] += r.v[i] >> 29;
-        r.v[i] &= M29;
+    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i];
+    if constexpr (kl(K) > 1) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            r.v[i + 1] += r.v[i] >> 29;
+            r.v[i] &= M29;
+        }
     }
-}
-
-// a + b  (fq: arith.rs:281-287 computes the same residue)
-template <int A, int B>
-BN_INLINE Fq<A + B> fq_add(const Fq<A>& a, const Fq<B>& b) {
-    Fq<A + B> r;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + b.v[i];
-    fq_normalize(r);
     return r;
 }
-template <int B>
-BN_INLINE Fq<2 * B> fq_dbl(const Fq<B>& a) { return fq_add(a, a); }
 
-// K*p with every digit but the top one raised into [2^29-1, 2^30): subtracting a
-// normalized value digit-wise from it never goes negative in digits 0..7; the top
-// digit is computed modulo 2^32 and is correct because the total is >= 0.
-constexpr Limbs9 kp_spread(int K) {
+// a + b, lazy (arith.rs:281-287 computes the same residue)
+template <int A, int B>
+BN_INLINE auto fq_add(const Fq<A>& a, const Fq<B>& b) {
+    if constexpr (kl(A) + kl(B) > kMaxLimb) {
+        if constexpr (kl(A) >= kl(B)) return fq_add(fq_norm(a), b); else return fq_add(a, fq_norm(b));
+    } else {
+        Fq<kenc(kv(A) + kv(B), kl(A) + kl(B))> r;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] + b.v[i];
+        return r;
+    }
+}
+template <int B>
+BN_INLINE auto fq_dbl(const Fq<B>& a) { return fq_add(a, a); }
+
+// K*p with digits raised so that subtracting any value with digit bound L
+// (digits < L*2^29) and value <= (K-1)*p leaves every digit non-negative:
+// digit i gets +(L+1)*2^29 and digit i+1 pays -(L+1) (net zero), and the top
+// digit keeps a margin of p/2^232 > 2^21 over the subtrahend's top digit.
+// Digits of the result are < (L+2)*2^29.
+constexpr Limbs9 kp_spread(int K, int L) {
     Limbs9 r = {{0, 0, 0, 0, 0, 0, 0, 0, 0}};
     unsigned long long c = 0;
     for (int i = 0; i < 9; ++i) {
@@ -108,43 +156,63 @@ constexpr Limbs9 kp_spread(int K) {
         r.v[i] = (uint32_t)(t & M29);
         c = t >> 29;
     }
-    r.v[0] += 1u << 29;
-    for (int i = 1; i < 8; ++i) r.v[i] += (1u << 29) - 1;
-    r.v[8] -= 1;
+    for (int i = 0; i < 8; ++i) {
+        r.v[i] += (uint32_t)(L + 1) << 29;
+        r.v[i + 1] -= (uint32_t)(L + 1);
+    }
     return r;
 }
 
-// a - b + B*p  (arith.rs:290-296 computes the same residue)
+// a - b + (B+1)*p, lazy (arith.rs:290-296 computes the same residue)
 template <int A, int B>
-BN_INLINE Fq<A + B> fq_sub(const Fq<A>& a, const Fq<B>& b) {
-    constexpr Limbs9 Q = kp_spread(B);
-    Fq<A + B> r;
+BN_INLINE auto fq_sub(const Fq<A>& a, const Fq<B>& b) {
+    if constexpr (kl(A) + kl(B) + 2 > kMaxLimb) {
+        if constexpr (kl(A) >= kl(B)) return fq_sub(fq_norm(a), b); else return fq_sub(a, fq_norm(b));
+    } else {
+        constexpr Limbs9 Q = kp_spread(kv(B) + 1, kl(B));
+        Fq<kenc(kv(A) + kv(B) + 1, kl(A) + kl(B) + 2)> r;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) r.v[i] = (a.v[i] + Q.v[i]) - b.v[i];
-    fq_normalize(r);
-    return r;
+        for (int i = 0; i < 9; ++i) r.v[i] = (a.v[i] + Q.v[i]) - b.v[i];
+        return r;
+    }
 }
-// B*p - a  (arith.rs:309-316: -0 stays 0, and B*p == 0 mod p)
-template <int B>
-BN_INLINE Fq<B> fq_neg(const Fq<B>& a) {
-    constexpr Limbs9 Q = kp_spread(B);
+// B*p - a, normalized, same bound (arith.rs:309-316: -0 stays 0, and B*p == 0 mod p)
+template <int K>
+BN_INLINE Fq<kv(K)> fq_neg(const Fq<K>& a_in) {
+    const Fq<kv(K)> a = fq_norm(a_in);
+    constexpr int B = kv(K);
+    // K*p with digits 0..7 raised into [2^29-1, 2^30); the top digit is taken
+    // modulo 2^32 and is right after the carry pass because the total is >= 0
+    constexpr Limbs9 Q = kp_spread(B, 0);
     Fq<B> r;
 #pragma unroll
     for (int i = 0; i < 9; ++i) r.v[i] = Q.v[i] - a.v[i];
-    fq_normalize(r);
-    return r;
+    return fq_norm(Fq<kenc(B, 2)>{{r.v[0], r.v[1], r.v[2], r.v[3], r.v[4], r.v[5], r.v[6], r.v[7], r.v[8]}});
 }
 
 // a * b * 2^-261 mod p: Montgomery product by finely integrated product
 // scanning.  Column k accumulates every a_i*b_j and m_i*p_j with i+j == k in a
-// 64-bit accumulator (18 products of < 2^58 each plus the carry-in stay below
-// 2^63), derives m_k = acc * (-p^-1) mod 2^29 for k < 9 so the low digit
-// cancels, then shifts by 29.  hipcc emits one v_mad_u64_u32 per product.
+// 64-bit accumulator (9 products < La*Lb*2^58, 9 < 2^58 and the carry-in stay
+// below 2^64 when La*Lb <= 6), derives m_k = acc * (-p^-1) mod 2^29 for k < 9
+// so the low digit cancels, then shifts by 29.  hipcc emits one v_mad_u64_u32
+// per product.  The result is normalized.
 template <int A, int B>
-BN_INLINE Fq<mul_bound(A, B)> fq_mul(const Fq<A>& a, const Fq<B>& b) {
-    static_assert((long long)A * B <= 160 * 160, "product bound");
+BN_INLINE auto fq_mul(const Fq<A>& a_in, const Fq<B>& b_in) {
+    if constexpr (kl(A) * kl(B) > 6) {
+        if constexpr (kl(A) >= kl(B)) return fq_mul(fq_norm(a_in), b_in); else return fq_mul(a_in, fq_norm(b_in));
+    } else {
+    static_assert((long long)kv(A) * kv(B) <= 160 * 160, "product bound");
+#if BN_FENCE_FQ
+    Fq<A> a = a_in;
+    Fq<B> b = b_in;
+    fq_fence(a);
+    fq_fence(b);
+#else
+    const Fq<A>& a = a_in;
+    const Fq<B>& b = b_in;
+#endif
     uint32_t m[9];
-    Fq<mul_bound(A, B)> r;
+    Fq<mul_bound(kv(A), kv(B))> r;
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 17; ++k) {
@@ -164,24 +232,42 @@ BN_INLINE Fq<mul_bound(A, B)> fq_mul(const Fq<A>& a, const Fq<B>& b) {
         acc >>= 29;
     }
     r.v[8] = (uint32_t)acc;
+#if BN_FENCE_FQ
+    fq_fence(r);
+#endif
     return r;
+    }
 }
 template <int B>
-BN_INLINE Fq<mul_bound(B, B)> fq_sqr(const Fq<B>& a) { return fq_mul(a, a); }
+BN_INLINE auto fq_sqr(const Fq<B>& a) { return fq_mul(a, a); }
 
 // bring any value back to bound 2 (a Montgomery product with one)
 template <int B>
-BN_INLINE Fq<mul_bound(B, 1)> fq_reduce(const Fq<B>& a) { return fq_mul(a, fq_one()); }
+BN_INLINE auto fq_reduce(const Fq<B>& a) { return fq_mul(a, fq_one()); }
 
-// x * c for a small constant c (digit-wise, then carry propagation)
+// x * c for a small constant c, lazy while the digits stay < 7*2^29; c == 8
+// on a normalized value (digits < 2^32) is carried at once
 template <int C, int B>
-BN_INLINE Fq<C * B> fq_mul_small(const Fq<B>& a) {
+BN_INLINE auto fq_mul_small(const Fq<B>& a) {
     static_assert(C >= 1 && C <= 8, "digit * C must fit 32 bits");
-    Fq<C * B> r;
+    if constexpr (kl(B) > 1 && C * kl(B) > kMaxLimb) {
+        return fq_mul_small<C>(fq_norm(a));
+    } else if constexpr (C * kl(B) > kMaxLimb) {  // C == 8, normalized input
+        Fq<C * kv(B)> o;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] * C;
-    fq_normalize(r);
-    return r;
+        for (int i = 0; i < 9; ++i) o.v[i] = a.v[i] * C;  // <= 8*(2^29-1): the carries fit
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            o.v[i + 1] += o.v[i] >> 29;
+            o.v[i] &= M29;
+        }
+        return o;
+    } else {
+        Fq<kenc(C * kv(B), C * kl(B))> r;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) r.v[i] = a.v[i] * C;
+        return r;
+    }
 }
 
 // Partial reduction to bound 2 without a multiplication: estimate

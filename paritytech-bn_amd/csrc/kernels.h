@@ -52,6 +52,37 @@ __device__ __forceinline__ Fq12<B> ld_fq12(const uint32_t* base, size_t n, size_
             {ld_fq2<B>(base, n, i, 6), ld_fq2<B>(base, n, i, 8), ld_fq2<B>(base, n, i, 10)}};
 }
 
+template <int B>
+__device__ __forceinline__ Fq6<B> ld_fq6(const uint32_t* base, size_t n, size_t i, int h) {
+    return {ld_fq2<B>(base, n, i, 6 * h), ld_fq2<B>(base, n, i, 6 * h + 2), ld_fq2<B>(base, n, i, 6 * h + 4)};
+}
+
+// Neither the machine scheduler nor the IR may move memory operations (or, for
+// the scheduler, anything) across this point: bounds the live ranges of a
+// long straight-line product so it fits the register file.
+__device__ __forceinline__ void sched_fence() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// a * [conj] b for b in lane-strided memory: fq12_mul's Karatsuba (fq12.rs
+// mul) with b loaded per Fq6 product instead of held, so only one operand,
+// the partial products and one Fq6 of b are live at a time.
+__device__ __forceinline__ Fq12<kF> mul12_mem(const Fq12<kF>& a, const uint32_t* b, size_t n, size_t i,
+                                              bool conj_b) {
+    const auto aa = fq6_fold(fq6_mul(a.c0, ld_fq6<kF>(b, n, i, 0)));
+    sched_fence();
+    Fq6<kF> b1 = ld_fq6<kF>(b, n, i, 1);
+    if (conj_b) b1 = fq6_neg(b1);
+    const auto bb = fq6_fold(fq6_mul(a.c1, b1));
+    const auto s = fq6_add(a.c0, a.c1);
+    sched_fence();
+    Fq6<kF> c1 = ld_fq6<kF>(b, n, i, 1);
+    if (conj_b) c1 = fq6_neg(c1);
+    const auto t = fq6_mul(s, fq6_add(ld_fq6<kF>(b, n, i, 0), c1));
+    return narrow12<kF>(mk12(fq6_add(fq6_mul_by_nonresidue(bb), aa), fq6_sub(fq6_sub(t, aa), bb)));
+}
+
 // ---------------------------------------------------------------- reference images
 __device__ __forceinline__ void ld_words(const bn_fq* src, uint32_t w[8]) {
     const uint4* s = reinterpret_cast<const uint4*>(src);

@@ -11,8 +11,8 @@ namespace bn {
 constexpr int kF = 4;
 template <int S, int B>
 BN_INLINE Fq12<S> narrow12(const Fq12<B>& a) {
-    if constexpr (B <= S) {
-        return widen<S>(a);
+    if constexpr (kv(B) <= S) {
+        return widen<S>(fq12_norm(a));
     } else {
         return widen<S>(fq12_fold(a));
     }

@@ -34,8 +34,8 @@ struct Fq12 {
 
 // ================================================================ Fq2 = Fq[u]/(u^2+1)
 template <int A, int B>
-BN_INLINE Fq2<cmax(A, B)> mk2(const Fq<A>& x, const Fq<B>& y) {
-    return {widen<cmax(A, B)>(x), widen<cmax(A, B)>(y)};
+BN_INLINE Fq2<kjoin(A, B)> mk2(const Fq<A>& x, const Fq<B>& y) {
+    return {widen<kjoin(A, B)>(x), widen<kjoin(A, B)>(y)};
 }
 template <int B2, int B>
 BN_INLINE Fq2<B2> widen(const Fq2<B>& a) { return {widen<B2>(a.c0), widen<B2>(a.c1)}; }
@@ -47,13 +47,13 @@ BN_INLINE Fq2<B> fq2_select(bool c, const Fq2<B>& a, const Fq2<B>& b) {
     return {fq_select(c, a.c0, b.c0), fq_select(c, a.c1, b.c1)};
 }
 template <int A, int B>
-BN_INLINE Fq2<A + B> fq2_add(const Fq2<A>& a, const Fq2<B>& b) { return {fq_add(a.c0, b.c0), fq_add(a.c1, b.c1)}; }
+BN_INLINE auto fq2_add(const Fq2<A>& a, const Fq2<B>& b) { return mk2(fq_add(a.c0, b.c0), fq_add(a.c1, b.c1)); }
 template <int A, int B>
-BN_INLINE Fq2<A + B> fq2_sub(const Fq2<A>& a, const Fq2<B>& b) { return {fq_sub(a.c0, b.c0), fq_sub(a.c1, b.c1)}; }
+BN_INLINE auto fq2_sub(const Fq2<A>& a, const Fq2<B>& b) { return mk2(fq_sub(a.c0, b.c0), fq_sub(a.c1, b.c1)); }
 template <int B>
-BN_INLINE Fq2<B> fq2_neg(const Fq2<B>& a) { return {fq_neg(a.c0), fq_neg(a.c1)}; }
+BN_INLINE auto fq2_neg(const Fq2<B>& a) { return mk2(fq_neg(a.c0), fq_neg(a.c1)); }
 template <int B>
-BN_INLINE Fq2<2 * B> fq2_dbl(const Fq2<B>& a) { return fq2_add(a, a); }
+BN_INLINE auto fq2_dbl(const Fq2<B>& a) { return fq2_add(a, a); }
 template <int B>
 BN_INLINE Fq2<2> fq2_fold(const Fq2<B>& a) { return {fq_fold(a.c0), fq_fold(a.c1)}; }
 template <int B>
@@ -61,14 +61,22 @@ BN_INLINE bool fq2_is_zero(const Fq2<B>& a) { return fq_is_zero(a.c0) & fq_is_ze
 // x unchanged when its bound is <= L, else folded to 2 (decided at compile time)
 template <int L, int B>
 BN_INLINE auto pre(const Fq<B>& a) {
-    if constexpr (B <= L) return a; else return fq_fold(a);
+    if constexpr (kv(B) <= L) return a; else return fq_fold(a);
 }
 template <int L, int B>
 BN_INLINE auto pre(const Fq2<B>& a) {
-    if constexpr (B <= L) return a; else return fq2_fold(a);
+    if constexpr (kv(B) <= L) return a; else return fq2_fold(a);
 }
 template <int A, int B>
 BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) { return fq_eq(a.c0, b.c0) & fq_eq(a.c1, b.c1); }
+
+template <int B>
+BN_INLINE Fq2<kv(B)> fq2_norm(const Fq2<B>& a) { return {fq_norm(a.c0), fq_norm(a.c1)}; }
+template <int B>
+BN_INLINE void fq2_fence(Fq2<B>& a) {
+    fq_fence(a.c0);
+    fq_fence(a.c1);
+}
 
 // fq2.rs:48-53
 template <int A, int B>
@@ -76,28 +84,38 @@ BN_INLINE auto fq2_scale(const Fq2<A>& a, const Fq<B>& s) { return mk2(fq_mul(a.
 
 // fq2.rs:136-148 (Karatsuba; bb * (p-1) + aa == aa - bb)
 template <int A, int B>
-BN_INLINE auto fq2_mul(const Fq2<A>& a, const Fq2<B>& b) {
-    if constexpr (A > 40 || B > 40) return fq2_mul(pre<40>(a), pre<40>(b)); else {
+BN_INLINE auto fq2_mul(const Fq2<A>& a_in, const Fq2<B>& b_in) {
+    if constexpr (kv(A) > 40 || kv(B) > 40) return fq2_mul(pre<40>(a_in), pre<40>(b_in)); else {
+    Fq2<A> a = a_in;
+    Fq2<B> b = b_in;
+    fq2_fence(a);
+    fq2_fence(b);
     auto aa = fq_mul(a.c0, b.c0);
     auto bb = fq_mul(a.c1, b.c1);
     auto t = fq_mul(fq_add(a.c0, a.c1), fq_add(b.c0, b.c1));
-    return mk2(fq_sub(aa, bb), fq_sub(fq_sub(t, aa), bb));
+    auto r = mk2(fq_sub(aa, bb), fq_sub(fq_sub(t, aa), bb));
+    fq2_fence(r);
+    return r;
     }
 }
 // fq2.rs:105-117: (c1*(p-1) + c0)(c0 + c1) - ab - ab*(p-1) == (c0 - c1)(c0 + c1); c1 = 2ab
 template <int A>
-BN_INLINE auto fq2_sqr(const Fq2<A>& a) {
-    if constexpr (A > 40) return fq2_sqr(fq2_fold(a)); else {
+BN_INLINE auto fq2_sqr(const Fq2<A>& a_in) {
+    if constexpr (kv(A) > 40) return fq2_sqr(fq2_fold(a_in)); else {
+    Fq2<A> a = a_in;
+    fq2_fence(a);
     auto ab = fq_mul(a.c0, a.c1);
     auto c0 = fq_mul(fq_sub(a.c0, a.c1), fq_add(a.c0, a.c1));
-    return mk2(c0, fq_dbl(ab));
+    auto r = mk2(c0, fq_dbl(ab));
+    fq2_fence(r);
+    return r;
     }
 }
 // x * xi, xi = 9 + u (fq2.rs:19-34, 55-57): (9a0 - a1) + (a0 + 9a1) u.
 // Inputs above bound 15 are folded first so the result stays <= 150.
 template <int A>
 BN_INLINE auto fq2_mul_xi(const Fq2<A>& a) {
-    if constexpr (A > 15) {
+    if constexpr (kv(A) > 15) {
         return fq2_mul_xi(fq2_fold(a));
     } else {
         auto n0 = fq_add(fq_mul_small<8>(a.c0), a.c0);
@@ -107,7 +125,7 @@ BN_INLINE auto fq2_mul_xi(const Fq2<A>& a) {
 }
 // fq2.rs:59-68: odd powers conjugate (c1 * (p-1) == -c1)
 template <int B>
-BN_INLINE Fq2<B> fq2_conj(const Fq2<B>& a) { return {a.c0, fq_neg(a.c1)}; }
+BN_INLINE auto fq2_conj(const Fq2<B>& a) { return mk2(a.c0, fq_neg(a.c1)); }
 
 // ---------------------------------------------------------------- inversion
 // Fermat: a^(p-2).  Inverses are unique, so this equals the reference's binary
@@ -141,8 +159,8 @@ BN_INLINE auto fq2_inv(const Fq2<B>& a_in) {
 
 // ================================================================ Fq6 = Fq2[v]/(v^3 - xi)
 template <int A, int B, int C>
-BN_INLINE Fq6<cmax(A, cmax(B, C))> mk6(const Fq2<A>& x, const Fq2<B>& y, const Fq2<C>& z) {
-    constexpr int M = cmax(A, cmax(B, C));
+BN_INLINE Fq6<kjoin(A, kjoin(B, C))> mk6(const Fq2<A>& x, const Fq2<B>& y, const Fq2<C>& z) {
+    constexpr int M = kjoin(A, kjoin(B, C));
     return {widen<M>(x), widen<M>(y), widen<M>(z)};
 }
 template <int B2, int B>
@@ -150,22 +168,24 @@ BN_INLINE Fq6<B2> widen(const Fq6<B>& a) { return {widen<B2>(a.c0), widen<B2>(a.
 BN_INLINE Fq6<1> fq6_zero() { return {fq2_zero(), fq2_zero(), fq2_zero()}; }
 BN_INLINE Fq6<1> fq6_one() { return {fq2_one(), fq2_zero(), fq2_zero()}; }
 template <int A, int B>
-BN_INLINE Fq6<A + B> fq6_add(const Fq6<A>& a, const Fq6<B>& b) {
-    return {fq2_add(a.c0, b.c0), fq2_add(a.c1, b.c1), fq2_add(a.c2, b.c2)};
+BN_INLINE auto fq6_add(const Fq6<A>& a, const Fq6<B>& b) {
+    return mk6(fq2_add(a.c0, b.c0), fq2_add(a.c1, b.c1), fq2_add(a.c2, b.c2));
 }
 template <int A, int B>
-BN_INLINE Fq6<A + B> fq6_sub(const Fq6<A>& a, const Fq6<B>& b) {
-    return {fq2_sub(a.c0, b.c0), fq2_sub(a.c1, b.c1), fq2_sub(a.c2, b.c2)};
+BN_INLINE auto fq6_sub(const Fq6<A>& a, const Fq6<B>& b) {
+    return mk6(fq2_sub(a.c0, b.c0), fq2_sub(a.c1, b.c1), fq2_sub(a.c2, b.c2));
 }
 template <int B>
-BN_INLINE Fq6<B> fq6_neg(const Fq6<B>& a) { return {fq2_neg(a.c0), fq2_neg(a.c1), fq2_neg(a.c2)}; }
+BN_INLINE auto fq6_neg(const Fq6<B>& a) { return mk6(fq2_neg(a.c0), fq2_neg(a.c1), fq2_neg(a.c2)); }
 template <int B>
 BN_INLINE Fq6<2> fq6_fold(const Fq6<B>& a) { return {fq2_fold(a.c0), fq2_fold(a.c1), fq2_fold(a.c2)}; }
+template <int B>
+BN_INLINE Fq6<kv(B)> fq6_norm(const Fq6<B>& a) { return {fq2_norm(a.c0), fq2_norm(a.c1), fq2_norm(a.c2)}; }
 template <int B>
 BN_INLINE bool fq6_is_zero(const Fq6<B>& a) { return fq2_is_zero(a.c0) & fq2_is_zero(a.c1) & fq2_is_zero(a.c2); }
 template <int L, int B>
 BN_INLINE auto pre(const Fq6<B>& a) {
-    if constexpr (B <= L) return a; else return fq6_fold(a);
+    if constexpr (kv(B) <= L) return a; else return fq6_fold(a);
 }
 // fq6.rs:109-115
 template <int B>
@@ -174,7 +194,7 @@ BN_INLINE auto fq6_mul_by_nonresidue(const Fq6<B>& a) { return mk6(fq2_mul_xi(a.
 // fq6.rs:197-207
 template <int A, int B>
 BN_INLINE auto fq6_mul(const Fq6<A>& a, const Fq6<B>& b) {
-    if constexpr (A > 20 || B > 20) return fq6_mul(pre<20>(a), pre<20>(b)); else {
+    if constexpr (kv(A) > 20 || kv(B) > 20) return fq6_mul(pre<20>(a), pre<20>(b)); else {
     auto a_a = fq2_mul(a.c0, b.c0);
     auto b_b = fq2_mul(a.c1, b.c1);
     auto c_c = fq2_mul(a.c2, b.c2);
@@ -187,7 +207,7 @@ BN_INLINE auto fq6_mul(const Fq6<A>& a, const Fq6<B>& b) {
 // fq6.rs:163-177
 template <int A>
 BN_INLINE auto fq6_sqr(const Fq6<A>& a) {
-    if constexpr (A > 20) return fq6_sqr(fq6_fold(a)); else {
+    if constexpr (kv(A) > 20) return fq6_sqr(fq6_fold(a)); else {
     auto s0 = fq2_sqr(a.c0);
     auto s1 = fq2_dbl(fq2_mul(a.c0, a.c1));
     auto s2 = fq2_sqr(fq2_add(fq2_sub(a.c0, a.c1), a.c2));
@@ -237,8 +257,8 @@ BN_INLINE auto fq6_frobenius_map(const Fq6<B>& a) {
 
 // ================================================================ Fq12 = Fq6[w]/(w^2 - v)
 template <int A, int B>
-BN_INLINE Fq12<cmax(A, B)> mk12(const Fq6<A>& x, const Fq6<B>& y) {
-    return {widen<cmax(A, B)>(x), widen<cmax(A, B)>(y)};
+BN_INLINE Fq12<kjoin(A, B)> mk12(const Fq6<A>& x, const Fq6<B>& y) {
+    return {widen<kjoin(A, B)>(x), widen<kjoin(A, B)>(y)};
 }
 template <int B2, int B>
 BN_INLINE Fq12<B2> widen(const Fq12<B>& a) { return {widen<B2>(a.c0), widen<B2>(a.c1)}; }
@@ -246,24 +266,26 @@ BN_INLINE Fq12<1> fq12_one() { return {fq6_one(), fq6_zero()}; }
 template <int B>
 BN_INLINE Fq12<2> fq12_fold(const Fq12<B>& a) { return {fq6_fold(a.c0), fq6_fold(a.c1)}; }
 template <int B>
+BN_INLINE Fq12<kv(B)> fq12_norm(const Fq12<B>& a) { return {fq6_norm(a.c0), fq6_norm(a.c1)}; }
+template <int B>
 BN_INLINE bool fq12_is_zero(const Fq12<B>& a) { return fq6_is_zero(a.c0) & fq6_is_zero(a.c1); }
 template <int L, int B>
 BN_INLINE auto pre(const Fq12<B>& a) {
-    if constexpr (B <= L) return a; else return fq12_fold(a);
+    if constexpr (kv(B) <= L) return a; else return fq12_fold(a);
 }
 template <int B>
-BN_INLINE Fq12<B> fq12_conj(const Fq12<B>& a) { return {a.c0, fq6_neg(a.c1)}; }  // unitary_inverse, fq12.rs:126-128
+BN_INLINE auto fq12_conj(const Fq12<B>& a) { return mk12(a.c0, fq6_neg(a.c1)); }  // unitary_inverse, fq12.rs:126-128
 template <int A, int B>
-BN_INLINE Fq12<A + B> fq12_add(const Fq12<A>& a, const Fq12<B>& b) { return {fq6_add(a.c0, b.c0), fq6_add(a.c1, b.c1)}; }
+BN_INLINE auto fq12_add(const Fq12<A>& a, const Fq12<B>& b) { return mk12(fq6_add(a.c0, b.c0), fq6_add(a.c1, b.c1)); }
 template <int A, int B>
-BN_INLINE Fq12<A + B> fq12_sub(const Fq12<A>& a, const Fq12<B>& b) { return {fq6_sub(a.c0, b.c0), fq6_sub(a.c1, b.c1)}; }
+BN_INLINE auto fq12_sub(const Fq12<A>& a, const Fq12<B>& b) { return mk12(fq6_sub(a.c0, b.c0), fq6_sub(a.c1, b.c1)); }
 template <int B>
-BN_INLINE Fq12<B> fq12_neg(const Fq12<B>& a) { return {fq6_neg(a.c0), fq6_neg(a.c1)}; }
+BN_INLINE auto fq12_neg(const Fq12<B>& a) { return mk12(fq6_neg(a.c0), fq6_neg(a.c1)); }
 
 // fq12.rs:319-327
 template <int A, int B>
 BN_INLINE auto fq12_mul(const Fq12<A>& a, const Fq12<B>& b) {
-    if constexpr (A > 10 || B > 10) return fq12_mul(pre<10>(a), pre<10>(b)); else {
+    if constexpr (kv(A) > 10 || kv(B) > 10) return fq12_mul(pre<10>(a), pre<10>(b)); else {
     auto aa = fq6_fold(fq6_mul(a.c0, b.c0));
     auto bb = fq6_fold(fq6_mul(a.c1, b.c1));
     auto t = fq6_mul(fq6_add(a.c0, a.c1), fq6_add(b.c0, b.c1));
@@ -273,7 +295,7 @@ BN_INLINE auto fq12_mul(const Fq12<A>& a, const Fq12<B>& b) {
 // fq12.rs:295-303
 template <int A>
 BN_INLINE auto fq12_sqr(const Fq12<A>& a) {
-    if constexpr (A > 2) return fq12_sqr(fq12_fold(a)); else {
+    if constexpr (kv(A) > 2) return fq12_sqr(fq12_fold(a)); else {
     auto ab = fq6_fold(fq6_mul(a.c0, a.c1));
     auto t = fq6_mul(fq6_add(fq6_mul_by_nonresidue(a.c1), a.c0), fq6_add(a.c0, a.c1));
     return mk12(fq6_sub(fq6_sub(t, ab), fq6_mul_by_nonresidue(ab)), fq6_add(ab, ab));
