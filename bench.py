@@ -33,9 +33,10 @@ sys.path.insert(0, ROOT)
 # Algorithmic work per pairing in generic Fq Montgomery products (SURVEY.md §8(d),
 # Appendix B: reference formulas with x(-1) and x xi folded into adds, inversions
 # excluded), per kernel phase of bn_pairing_many_dev.
-# k_fq12_vm: the reference's 8767 less the 12 Fq12 products (54 each) the signed-digit
-# (NAF) chains for u save: the work counted is the work the kernel does.
-FQMUL_PER_PAIRING = {"k_prepare": 19 + 2655, "k_miller": 6045, "k_fq12_vm": 8767 - 12 * 54, "k_fe_out": 0}
+# k_fq12_vm: the reference's 8767 less what the width-4 signed-window chains for u
+# save per exp_by_neg_z (16 Fq12 products instead of 27, one extra cyclotomic
+# square of 18): the work counted is the work the kernel does.
+FQMUL_PER_PAIRING = {"k_prepare": 19 + 2655, "k_miller": 6045, "k_fq12_vm": 8767 - 3 * (11 * 54 - 18), "k_fe_out": 0}
 MAD32_PER_FQMUL = 128  # one 8x32-bit CIOS product: 64 (a*b) + 64 (m*p) v_mad_u64_u32
 # gfx950 integer-VALU peak for v_mad_u64_u32: 4 cycles per wave64 instruction (measured,
 # tools/ubench.hip) = 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  ubench sustains 34.7 T/s.

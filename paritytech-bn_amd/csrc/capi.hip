@@ -69,47 +69,67 @@ struct Prog {
         s.push_back(w[0]);
         s.push_back(w[1]);
     }
-    // x^e for a signed-digit chain (digit, position) from the top digit (+1)
-    // down, each run "square k times, multiply by x or conj(x)" as one step;
-    // the last step conjugates when `conj_out`.
-    uint32_t chain(uint32_t x, const std::vector<std::pair<int, int>>& digits, bool conj_out) {
+    // x^e for a signed-digit chain (digit, position), top digit first and
+    // positive.  pow[d] is the slot holding x^d for each odd |d| used; each run
+    // "square k times, multiply by x^|d| or its conjugate" is one step, and the
+    // last step conjugates when `conj_out`.
+    uint32_t chain(const uint32_t* pow, const std::vector<std::pair<int, int>>& digits, bool conj_out) {
         const uint32_t r = tmp();
         int pos = digits[0].second;
-        uint32_t src = x;
+        uint32_t src = pow[digits[0].first];
+        bool wrote = false;
         for (size_t t = 1; t < digits.size(); ++t) {
+            const int d = digits[t].first;
             const bool last = t + 1 == digits.size() && digits[t].second == 0;
-            op(OP_MUL, r, src, x, (uint32_t)(pos - digits[t].second),
-               (digits[t].first < 0 ? kFlagConjB : 0) | (last && conj_out ? kFlagConjOut : 0));
+            op(OP_MUL, r, src, pow[d < 0 ? -d : d], (uint32_t)(pos - digits[t].second),
+               (d < 0 ? kFlagConjB : 0) | (last && conj_out ? kFlagConjOut : 0));
             pos = digits[t].second;
             src = r;
+            wrote = true;
         }
         if (pos > 0) {
             op(OP_CYC, r, src, 0, (uint32_t)pos);
             if (conj_out) op(OP_CONJ, r, r);
-        } else if (src == x) {  // a single digit at position 0: x itself
-            op(conj_out ? OP_CONJ : OP_MOV, r, x);
+        } else if (!wrote) {  // a single digit at position 0
+            op(conj_out ? OP_CONJ : OP_MOV, r, src);
         }
         return r;
     }
     // exp_by_neg_z, fq12.rs:121-124: conj(cyclotomic_pow(u)) with
-    // u = 0x44e992b44a6909f1 (fq12.rs:249-266).  `naf` = use the 24-digit
-    // signed form of u, valid when x is in the cyclotomic subgroup (there
-    // conj(x) = x^-1) -- always true inside the final exponentiation; the
-    // generic op (bn_fq12_op_many) keeps the reference's binary chain so its
-    // output matches the reference for any input.
-    uint32_t exp_by_neg_z(uint32_t x, bool naf = false) {
+    // u = 0x44e992b44a6909f1 (fq12.rs:249-266).
+    // windowed = width-4 signed window (digits +-1, 3, 5, 7: 13 chain products
+    // + 3 for x^3, x^5, x^7, instead of the 27 of the binary chain), valid when
+    // x is in the cyclotomic subgroup (there conj(x) = x^-1) -- always true
+    // inside the final exponentiation.  The generic op (bn_fq12_op_many) keeps
+    // the reference's binary chain so its output matches for any input.
+    uint32_t exp_by_neg_z(uint32_t x, bool windowed = false) {
+        constexpr int W = 4;
         uint64_t u = 4965661367192848881ull;
         std::vector<std::pair<int, int>> d;  // (digit, position), low to high
         for (int pos = 0; u; ++pos, u >>= 1) {
             if (!(u & 1)) continue;
             int z = 1;
-            if (naf && (u & 3) == 3) z = -1;
+            if (windowed) {
+                z = (int)(u & ((1u << W) - 1));
+                if (z >= (1 << (W - 1))) z -= 1 << W;
+            }
             d.push_back({z, pos});
-            u -= (uint64_t)(int64_t)z;  // u - z is even
+            u -= (uint64_t)(int64_t)z;  // u - z is divisible by 2^W (or 2)
         }
         std::reverse(d.begin(), d.end());
-        return chain(x, d, true);
+        uint32_t pow[1 << (W - 1)] = {0};
+        pow[1] = x;
+        if (windowed) {
+            if (!win2) win2 = tmp(), win[3] = tmp(), win[5] = tmp(), win[7] = tmp();  // shared by the three calls
+            op(OP_CYC, win2, x, 0, 1);
+            op(OP_MUL, win[3], x, win2);
+            op(OP_MUL, win[5], win[3], win2);
+            op(OP_MUL, win[7], win[5], win2);
+            pow[3] = win[3], pow[5] = win[5], pow[7] = win[7];
+        }
+        return chain(pow, d, true);
     }
+    uint32_t win2 = 0, win[8] = {0};
 };
 // final_exponentiation (fq12.rs:107-110) of slot 0; returns the result slot.
 // Same operations as the reference; conjugations ride on the multiplies.
