@@ -130,6 +130,34 @@ struct Prog {
         return chain(pow, d, true);
     }
     uint32_t win2 = 0, win[8] = {0};
+    // Register forwarding: a step whose operand a is the previous step's
+    // destination reads it from registers (kFlagAccA); a result that no later
+    // step reads from its slot, and that is not a program output still in
+    // place at the end, is not stored (kFlagNoStore).
+    void finalize(const std::vector<uint32_t>& outputs) {
+        const int n = steps();
+        auto D = [&](int t) { return (s[2 * t] >> 8) & 0xff; };
+        auto A = [&](int t) { return (s[2 * t] >> 16) & 0xff; };
+        auto Bo = [&](int t) { return s[2 * t] >> 24; };
+        auto reads_b = [&](int t) { return (s[2 * t] & 0xff) == OP_MUL; };
+        for (int t = 1; t < n; ++t)
+            if (A(t) == D(t - 1)) s[2 * t + 1] |= kFlagAccA << 8;
+        for (int t = 0; t < n; ++t) {
+            const uint32_t d = D(t);
+            bool needed = true;  // stays true if d is an output never overwritten
+            bool overwritten = false;
+            bool read = false;
+            for (int u = t + 1; u < n && !overwritten; ++u) {
+                const bool via_acc = u == t + 1 && ((s[2 * u + 1] >> 8) & kFlagAccA);
+                if ((A(u) == d && !via_acc) || (reads_b(u) && Bo(u) == d)) read = true;
+                if (D(u) == d) overwritten = true;
+            }
+            bool is_out = false;
+            for (uint32_t o : outputs) is_out |= o == d;
+            needed = read || (is_out && !overwritten);
+            if (!needed) s[2 * t + 1] |= kFlagNoStore << 8;
+        }
+    }
 };
 // final_exponentiation (fq12.rs:107-110) of slot 0; returns the result slot.
 // Same operations as the reference; conjugations ride on the multiplies.
@@ -274,6 +302,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
     c->device = device;
     Prog P;
     c->fe_out = (int)build_final_exp(P);
+    P.finalize({(uint32_t)c->fe_out});
     c->fe_steps = P.steps();
     if (P.next > (uint32_t)kFeSlots) {
         delete c;
@@ -596,6 +625,7 @@ int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n,
             case BN_FQ12_FROB2: P.op(OP_FROB2, res, 1); break;
             default: P.op(OP_FROB3, res, 1); break;
         }
+        P.finalize({res});
         HIPCHK(c, hipMemcpyAsync(dprog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice, c->stream));
         k_fq12_vm<<<grid_for(m), kBlock, 0, c->stream>>>(dprog, P.steps(), c->slots, m);
         k_gt_store<<<grid_for(m), kBlock, 0, c->stream>>>(c->slots + (size_t)res * kSlotWords * m, m, m, dout);

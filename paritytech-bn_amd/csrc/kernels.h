@@ -186,12 +186,15 @@ inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock
 // OP_CYC:  d = cyc^k(a)                       (k cyclotomic squarings in registers)
 // OP_MUL:  d = [conj] (cyc^k(a) * [conj] b)   (kFlagConjB, kFlagConjOut)
 // so a whole run of an exponent chain (zeros then a digit) is one step and the
-// slot traffic is paid once per nonzero digit, not once per squaring.
+// slot traffic is paid once per nonzero digit, not once per squaring.  The
+// previous step's result stays in registers: kFlagAccA takes operand a from
+// there instead of its slot, and kFlagNoStore skips the store of a result that
+// no later step reads from its slot.
 enum Fq12Op : uint32_t {
     OP_MOV = 0, OP_MUL = 1, OP_SQR = 2, OP_CYC = 3, OP_CONJ = 4,
     OP_FROB1 = 5, OP_FROB2 = 6, OP_FROB3 = 7, OP_INV = 8
 };
-constexpr uint32_t kFlagConjB = 1, kFlagConjOut = 2;
+constexpr uint32_t kFlagConjB = 1, kFlagConjOut = 2, kFlagAccA = 4, kFlagNoStore = 8;
 constexpr int kSlotWords = 108;  // 12 Fq x 9 digits
 inline void vm_step(uint32_t out[2], uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t k, uint32_t flags) {
     out[0] = op | (d << 8) | (a << 16) | (b << 24);

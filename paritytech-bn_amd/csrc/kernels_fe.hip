@@ -12,6 +12,7 @@ __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__
                                                     size_t n) {
     const size_t i = lane_id();
     if (i >= n) return;
+    Fq12<kF> acc = widen<kF>(fq12_one());  // the previous step's result, kept in registers
 #pragma unroll 1
     for (int pc = 0; pc < nsteps; ++pc) {
         const uint32_t ins = prog[2 * pc];  // uniform: scalar loads
@@ -20,33 +21,35 @@ __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__
         uint32_t* d = slot_ptr(slots, n, (ins >> 8) & 0xff);
         const uint32_t* a = slot_ptr(slots, n, (ins >> 16) & 0xff);
         const uint32_t* b = slot_ptr(slots, n, ins >> 24);
+        Fq12<kF> x;
+        if (flags & kFlagAccA) x = acc; else x = ld_fq12<kF>(a, n, i);
+        Fq12<kF> r;
         switch (op) {
-            case OP_MOV: st_fq12(d, n, i, ld_fq12<kF>(a, n, i)); break;
+            case OP_MOV: r = x; break;
             case OP_MUL: {
-                Fq12<kF> x = ld_fq12<kF>(a, n, i);
 #pragma unroll 1
                 for (uint32_t j = 0; j < k; ++j) x = cyc_sqr(x);
                 Fq12<kF> y = ld_fq12<kF>(b, n, i);
                 if (flags & kFlagConjB) y = fq12_conj(y);
-                Fq12<kF> r = mul12(x, y);
+                r = mul12(x, y);
                 if (flags & kFlagConjOut) r = fq12_conj(r);
-                st_fq12(d, n, i, r);
                 break;
             }
-            case OP_SQR: st_fq12(d, n, i, narrow12<kF>(fq12_sqr(ld_fq12<kF>(a, n, i)))); break;
+            case OP_SQR: r = narrow12<kF>(fq12_sqr(x)); break;
             case OP_CYC: {
-                Fq12<kF> x = ld_fq12<kF>(a, n, i);
 #pragma unroll 1
                 for (uint32_t j = 0; j < k; ++j) x = cyc_sqr(x);
-                st_fq12(d, n, i, x);
+                r = x;
                 break;
             }
-            case OP_CONJ: st_fq12(d, n, i, fq12_conj(ld_fq12<kF>(a, n, i))); break;
-            case OP_FROB1: st_fq12(d, n, i, narrow12<kF>(fq12_frobenius_map<1>(ld_fq12<kF>(a, n, i)))); break;
-            case OP_FROB2: st_fq12(d, n, i, narrow12<kF>(fq12_frobenius_map<2>(ld_fq12<kF>(a, n, i)))); break;
-            case OP_FROB3: st_fq12(d, n, i, narrow12<kF>(fq12_frobenius_map<3>(ld_fq12<kF>(a, n, i)))); break;
-            default: st_fq12(d, n, i, narrow12<kF>(fq12_inv(ld_fq12<kF>(a, n, i)))); break;  // OP_INV
+            case OP_CONJ: r = fq12_conj(x); break;
+            case OP_FROB1: r = narrow12<kF>(fq12_frobenius_map<1>(x)); break;
+            case OP_FROB2: r = narrow12<kF>(fq12_frobenius_map<2>(x)); break;
+            case OP_FROB3: r = narrow12<kF>(fq12_frobenius_map<3>(x)); break;
+            default: r = narrow12<kF>(fq12_inv(x)); break;  // OP_INV
         }
+        acc = r;
+        if (!(flags & kFlagNoStore)) st_fq12(d, n, i, r);
     }
 }
 
