@@ -163,6 +163,9 @@ constexpr Limbs9 kp_spread(int K, int L) {
     return r;
 }
 
+// the normalized digits of K*p
+constexpr Limbs9 kp_plain(int K) { return kp_spread(K, -1); }
+
 // a - b + (B+1)*p, lazy (arith.rs:290-296 computes the same residue)
 template <int A, int B>
 BN_INLINE auto fq_sub(const Fq<A>& a, const Fq<B>& b) {

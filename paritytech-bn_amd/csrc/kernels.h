@@ -14,6 +14,7 @@ namespace bn {
 constexpr int kBlock = 256;
 constexpr int kCoeffFq = BN_NUM_COEFFS * 6;  // Fq elements of line coefficients per pairing
 constexpr size_t kChunk = size_t(1) << 18;   // pairings per launch set (~5 GB workspace)
+constexpr int kSlotWords = 108;              // one Fq12: 12 Fq x 9 digits
 
 // ---------------------------------------------------------------- lane-strided storage
 template <int B>
@@ -57,31 +58,78 @@ __device__ __forceinline__ Fq6<B> ld_fq6(const uint32_t* base, size_t n, size_t 
     return {ld_fq2<B>(base, n, i, 6 * h), ld_fq2<B>(base, n, i, 6 * h + 2), ld_fq2<B>(base, n, i, 6 * h + 4)};
 }
 
-// Neither the machine scheduler nor the IR may move memory operations (or, for
-// the scheduler, anything) across this point: bounds the live ranges of a
-// long straight-line product so it fits the register file.
-__device__ __forceinline__ void sched_fence() {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
+// No memory operation may move across this point (compiler barrier only).
+__device__ __forceinline__ void mem_fence() { asm volatile("" ::: "memory"); }
+
+// Fq6 product (fq6.rs:197-207, the same Karatsuba as fq6_mul) with operand b
+// supplied per Fq2 coordinate by g(j), fetched right before each product that
+// needs it (mem_fence keeps the loads from being hoisted), so b never has to be
+// held in registers.
+template <int A, class G>
+__device__ __forceinline__ auto fq6_mul_g(const Fq6<A>& a, G&& g) {
+    if constexpr (kv(A) > 20) {
+        return fq6_mul_g(fq6_fold(a), g);
+    } else {
+        mem_fence();
+        auto a_a = fq2_mul(a.c0, g(0));
+        mem_fence();
+        auto b_b = fq2_mul(a.c1, g(1));
+        mem_fence();
+        auto c_c = fq2_mul(a.c2, g(2));
+        mem_fence();
+        auto t0 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c1, a.c2), fq2_add(g(1), g(2))), b_b), c_c);
+        mem_fence();
+        auto t1 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c0, a.c1), fq2_add(g(0), g(1))), a_a), b_b);
+        mem_fence();
+        auto t2 = fq2_sub(fq2_mul(fq2_add(a.c0, a.c2), fq2_add(g(0), g(2))), a_a);
+        return mk6(fq2_add(fq2_mul_xi(t0), a_a), fq2_add(t1, fq2_mul_xi(c_c)), fq2_sub(fq2_add(t2, b_b), c_c));
+    }
 }
 
-// a * [conj] b for b in lane-strided memory: fq12_mul's Karatsuba (fq12.rs
-// mul) with b loaded per Fq6 product instead of held, so only one operand,
-// the partial products and one Fq6 of b are live at a time.
-__device__ __forceinline__ Fq12<kF> mul12_mem(const Fq12<kF>& a, const uint32_t* b, size_t n, size_t i,
-                                              bool conj_b) {
-    const auto aa = fq6_fold(fq6_mul(a.c0, ld_fq6<kF>(b, n, i, 0)));
-    sched_fence();
-    Fq6<kF> b1 = ld_fq6<kF>(b, n, i, 1);
-    if (conj_b) b1 = fq6_neg(b1);
-    const auto bb = fq6_fold(fq6_mul(a.c1, b1));
+// a * b (fq12.rs:319-327 Karatsuba) with b read per Fq2 from `yl`, the calling
+// lane's lane-strided copy of an Fq12 in LDS (word w at yl[w * kBlock]);
+// conj_b multiplies by conj(b) instead (fq12.rs:126-128).
+__device__ __forceinline__ Fq12<kF> mul12_lds(const Fq12<kF>& a, const uint32_t* yl, bool conj_b) {
+    auto ld = [&](int j) {  // Fq2 coordinate j of b (0..2: b.c0, 3..5: b.c1)
+        Fq2<kF> r;
+#pragma unroll
+        for (int l = 0; l < 9; ++l) {
+            r.c0.v[l] = yl[((2 * j) * 9 + l) * kBlock];
+            r.c1.v[l] = yl[((2 * j + 1) * 9 + l) * kBlock];
+        }
+        return r;
+    };
+    auto g0 = [&](int j) { return ld(j); };
+    auto g1 = [&](int j) {
+        Fq2<kF> r = ld(3 + j);
+        if (conj_b) r = fq2_neg(r);
+        return r;
+    };
+    auto gs = [&](int j) { return fq2_add(g0(j), g1(j)); };
+    const auto aa = fq6_fold(fq6_mul_g(a.c0, g0));
     const auto s = fq6_add(a.c0, a.c1);
-    sched_fence();
-    Fq6<kF> c1 = ld_fq6<kF>(b, n, i, 1);
-    if (conj_b) c1 = fq6_neg(c1);
-    const auto t = fq6_mul(s, fq6_add(ld_fq6<kF>(b, n, i, 0), c1));
+    const auto bb = fq6_fold(fq6_mul_g(a.c1, g1));
+    const auto t = fq6_mul_g(s, gs);
     return narrow12<kF>(mk12(fq6_add(fq6_mul_by_nonresidue(bb), aa), fq6_sub(fq6_sub(t, aa), bb)));
 }
+
+// Asynchronous copy of a lane-strided Fq12 (108 words, stride n) from global
+// memory into the block's LDS image (stride kBlock) with buffer_load ... lds:
+// no VGPRs and no vector ALU (SGPR offsets, M0 = the wave's LDS base).  The
+// caller waits with lds_copy_wait() before reading.
+__device__ __forceinline__ void lds_copy_fq12(const uint32_t* src_block, size_t n, uint32_t* yl_block) {
+    // src_block = slot base + blockIdx.x * kBlock; yl_block = LDS image base
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src_block, 0, 0x7fffffff, 0x00020000);
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    const int lane_off = (int)(threadIdx.x & 63u) * 4 + (int)wave * 4;
+#pragma unroll
+    for (int w = 0; w < kSlotWords; ++w)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(yl_block + w * kBlock + wave), 4, lane_off,
+            (int)((size_t)w * n * 4), 0, 0);
+}
+__device__ __forceinline__ void lds_copy_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------- reference images
 __device__ __forceinline__ void ld_words(const bn_fq* src, uint32_t w[8]) {
@@ -195,7 +243,6 @@ enum Fq12Op : uint32_t {
     OP_FROB1 = 5, OP_FROB2 = 6, OP_FROB3 = 7, OP_INV = 8
 };
 constexpr uint32_t kFlagConjB = 1, kFlagConjOut = 2, kFlagAccA = 4, kFlagNoStore = 8;
-constexpr int kSlotWords = 108;  // 12 Fq x 9 digits
 inline void vm_step(uint32_t out[2], uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t k, uint32_t flags) {
     out[0] = op | (d << 8) | (a << 16) | (b << 24);
     out[1] = k | (flags << 8);

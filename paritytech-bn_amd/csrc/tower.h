@@ -82,7 +82,77 @@ BN_INLINE void fq2_fence(Fq2<B>& a) {
 template <int A, int B>
 BN_INLINE auto fq2_scale(const Fq2<A>& a, const Fq<B>& s) { return mk2(fq_mul(a.c0, s), fq_mul(a.c1, s)); }
 
-// fq2.rs:136-148 (Karatsuba; bb * (p-1) + aa == aa - bb)
+// Fq2 product with one Montgomery reduction per output coordinate (lazy
+// reduction): per column k of the schoolbook products P = a0*b0, Q = a1*b1 and
+// T = (a0+a1)*(b0+b1) are summed unreduced, and the two coordinates
+//   c0 = REDC(P - Q)          (signed 64-bit columns)
+//   c1 = REDC(T - P - Q)      (= a0*b1 + a1*b0 >= 0, unsigned columns)
+// are reduced in the same column loop: 3*81 + 2*81 multiply-adds instead of
+// 3*162.  Column bounds: |P - Q| + m*p < 27*2^58 < 2^63 and the c1 column
+// < 45*2^58 < 2^64 when La*Lb <= 2 (T may wrap mod 2^64 mid-sum; the final
+// column value is exact).  c0 may come out negative (> -A*B*p^2/R): a multiple
+// of p is added back.
+// K0 with K0*p > A*B*p^2/R by at least p/2 (so the top digit of c0 + K0*p is >= 0)
+constexpr int fq2_neg_margin(int A, int B) { return 2 + (int)(((long long)A * B * 5908) / 1000000); }
+template <int A, int B>
+BN_INLINE auto fq2_mul_lazy(const Fq2<A>& a, const Fq2<B>& b) {
+    if constexpr (kl(A) * kl(B) > 2) {
+        if constexpr (kl(A) >= kl(B)) return fq2_mul_lazy(fq2_norm(a), b); else return fq2_mul_lazy(a, fq2_norm(b));
+    } else {
+    static_assert(kv(A) <= 40 && kv(B) <= 40, "fq2_mul_lazy bound");
+    constexpr int K0 = fq2_neg_margin(kv(A), kv(B));
+    constexpr int B0 = mul_bound(kv(A), kv(B)) + K0;
+    constexpr int B1 = 1 + (int)(((long long)2 * kv(A) * kv(B) * 5908 + 999999) / 1000000);
+    const auto s = fq_add(a.c0, a.c1);
+    const auto t = fq_add(b.c0, b.c1);
+    uint32_t m0[9], m1[9];
+    Fq<kenc(B0, 2)> c0;
+    Fq<B1> c1;
+    int64_t acc0 = 0;
+    uint64_t acc1 = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        const int lo = k < 9 ? 0 : k - 8;
+        const int hi = k < 9 ? k : 8;
+        uint64_t P = 0, Q = 0;
+#pragma unroll
+        for (int i = lo; i <= hi; ++i) {
+            P += (uint64_t)a.c0.v[i] * b.c0.v[k - i];
+            Q += (uint64_t)a.c1.v[i] * b.c1.v[k - i];
+            acc1 += (uint64_t)s.v[i] * t.v[k - i];
+        }
+        acc0 += (int64_t)(P - Q);
+        acc1 -= P + Q;
+#pragma unroll
+        for (int i = lo; i <= hi; ++i) {
+            if (i < k) {
+                acc0 += (int64_t)((uint64_t)m0[i] * kP29.v[k - i]);
+                acc1 += (uint64_t)m1[i] * kP29.v[k - i];
+            }
+        }
+        if (k < 9) {
+            m0[k] = ((uint32_t)acc0 * BN_PINV29) & M29;
+            m1[k] = ((uint32_t)acc1 * BN_PINV29) & M29;
+            acc0 += (int64_t)((uint64_t)m0[k] * kP29.v[0]);
+            acc1 += (uint64_t)m1[k] * kP29.v[0];
+        } else {
+            c0.v[k - 9] = (uint32_t)acc0 & M29;
+            c1.v[k - 9] = (uint32_t)acc1 & M29;
+        }
+        acc0 >>= 29;  // arithmetic
+        acc1 >>= 29;
+    }
+    // c0 + K0*p: digits 0..7 < 2^30, the (signed) top digit becomes >= 0
+    constexpr Limbs9 KP = kp_plain(K0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) c0.v[i] += KP.v[i];
+    c0.v[8] = (uint32_t)acc0 + KP.v[8];
+    c1.v[8] = (uint32_t)acc1;
+    return mk2(c0, c1);
+    }
+}
+
+// fq2.rs:136-148: the same product (Karatsuba, bb * (p-1) + aa == aa - bb)
 template <int A, int B>
 BN_INLINE auto fq2_mul(const Fq2<A>& a_in, const Fq2<B>& b_in) {
     if constexpr (kv(A) > 40 || kv(B) > 40) return fq2_mul(pre<40>(a_in), pre<40>(b_in)); else {
@@ -90,10 +160,7 @@ BN_INLINE auto fq2_mul(const Fq2<A>& a_in, const Fq2<B>& b_in) {
     Fq2<B> b = b_in;
     fq2_fence(a);
     fq2_fence(b);
-    auto aa = fq_mul(a.c0, b.c0);
-    auto bb = fq_mul(a.c1, b.c1);
-    auto t = fq_mul(fq_add(a.c0, a.c1), fq_add(b.c0, b.c1));
-    auto r = mk2(fq_sub(aa, bb), fq_sub(fq_sub(t, aa), bb));
+    auto r = fq2_mul_lazy(a, b);
     fq2_fence(r);
     return r;
     }
@@ -112,10 +179,10 @@ BN_INLINE auto fq2_sqr(const Fq2<A>& a_in) {
     }
 }
 // x * xi, xi = 9 + u (fq2.rs:19-34, 55-57): (9a0 - a1) + (a0 + 9a1) u.
-// Inputs above bound 15 are folded first so the result stays <= 150.
+// Inputs above bound 8 are folded first so the result stays <= 82.
 template <int A>
 BN_INLINE auto fq2_mul_xi(const Fq2<A>& a) {
-    if constexpr (kv(A) > 15) {
+    if constexpr (kv(A) > 8) {
         return fq2_mul_xi(fq2_fold(a));
     } else {
         auto n0 = fq_add(fq_mul_small<8>(a.c0), a.c0);

@@ -22,6 +22,11 @@ template <int OP>
 __global__ void __launch_bounds__(kBlock) k_reg(uint32_t* slots, size_t n, int reps) {
     const size_t i = lane_id();
     if (i >= n) return;
+    __shared__ uint32_t yl[kSlotWords * kBlock];
+    if constexpr (OP == 3) {
+        lds_copy_fq12(slots + kSlotWords * n + (size_t)blockIdx.x * kBlock, n, yl);
+        lds_copy_wait();
+    }
     Fq12<kF> x = ld_fq12<kF>(slots, n, i);
     const Fq12<kF> y = ld_fq12<kF>(slots + kSlotWords * n, n, i);
 #pragma unroll 1
@@ -29,7 +34,23 @@ __global__ void __launch_bounds__(kBlock) k_reg(uint32_t* slots, size_t n, int r
         if constexpr (OP == 0) x = mul12(x, y);
         if constexpr (OP == 1) x = cyc_sqr(x);
         if constexpr (OP == 2) x = narrow12<kF>(fq12_sqr(x));
-        if constexpr (OP == 3) x = mul12_mem(x, slots + kSlotWords * n, n, i, false);
+        if constexpr (OP == 3) x = mul12_lds(x, yl + threadIdx.x, false);
+    }
+    st_fq12(slots + 2 * kSlotWords * n, n, i, x);
+}
+// the same operations compiled for two resident waves per SIMD (<= 256 registers)
+template <int OP>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_reg2(uint32_t* slots, size_t n, int reps) {
+    const size_t i = lane_id();
+    if (i >= n) return;
+    Fq12<kF> x = ld_fq12<kF>(slots, n, i);
+    const Fq12<kF> y = ld_fq12<kF>(slots + kSlotWords * n, n, i);
+#pragma unroll 1
+    for (int r = 0; r < reps; ++r) {
+        if constexpr (OP == 0) x = mul12(x, y);
+        if constexpr (OP == 1) x = cyc_sqr(x);
+        if constexpr (OP == 2) x = narrow12<kF>(fq12_sqr(x));
     }
     st_fq12(slots + 2 * kSlotWords * n, n, i, x);
 }
@@ -115,6 +136,9 @@ int main(int argc, char** argv) {
     time_reg("reg mul12", k_reg<0>);
     time_reg("reg cyc_sqr", k_reg<1>);
     time_reg("reg fq12_sqr", k_reg<2>);
-    time_reg("reg mul12_mem (b from memory)", k_reg<3>);
+    time_reg("reg mul12_lds (b from LDS)", k_reg<3>);
+    time_reg("reg2 cyc_sqr (<=256 regs)", k_reg2<1>);
+    time_reg("reg2 fq12_sqr (<=256 regs)", k_reg2<2>);
+    time_reg("reg2 mul12 (<=256 regs)", k_reg2<0>);
     return 0;
 }
