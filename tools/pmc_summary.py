@@ -1,27 +1,71 @@
 #!/usr/bin/env python3
-"""Summarize rocprofv3 --pmc CSVs (separate FETCH_SIZE / WRITE_SIZE / SQ passes)
-into profiles/pmc_summary.json (read by bench.py for roofline.traffic) and a
-text table.  FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  Per
-MI355X_MICROARCH.md §HBM, FETCH_SIZE reads half the bytes of 16-B/lane streaming
-loads; this engine's loads are 4-B/lane dwords (uncalibrated), so the raw value
-is reported and the caveat recorded."""
+"""Summarize one gpu_round.sh session (rocprofv3 sqlite output, ROCm 7.2).
+
+    python tools/pmc_summary.py gpurun_out/TAG TAG
+
+Reads  TAG/prof/run_results.db                    (--kernel-trace --stats pass)
+       TAG/pmc_{fetch,write,sq}/p_results.db      (one --pmc pass each)
+Writes profiles/TAG_kernel_stats.csv              (per-kernel launches, average / min / max ns)
+       profiles/TAG_pmc.txt                       (per-kernel counter table)
+       profiles/pmc_summary.json                  (bench.py reads roofline.traffic from it)
+
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  Per MI355X_MICROARCH.md §HBM,
+FETCH_SIZE counts half the bytes of 16-B/lane streaming reads; this engine's
+workspace accesses are 4-B/lane coalesced dwords (256 B per wave instruction),
+an access width the guide lists as uncalibrated, so the raw value x 1024 is
+reported and the caveat recorded with it.
+"""
 import collections
 import csv
+import glob
 import json
 import os
+import sqlite3
 import sys
 
-src, tag = sys.argv[1], sys.argv[2]  # e.g. gpurun_out r1
+src, tag = sys.argv[1], sys.argv[2]
 out_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles")
+
+
+def short(name):
+    return name.split("(")[0].replace("bn::", "")
+
+
+def one_db(pattern):
+    hits = sorted(glob.glob(os.path.join(src, pattern)))
+    return sqlite3.connect(hits[0]) if hits else None
+
+
+# ---- kernel stats
+db = one_db("prof/*results.db")
+rows = []
+if db is not None:
+    per = collections.defaultdict(list)
+    for name, dur in db.execute("select name, duration from kernels"):
+        per[name].append(dur)
+    with open(os.path.join(out_dir, "%s_kernel_stats.csv" % tag), "w", newline="") as fh:
+        w = csv.writer(fh, quoting=csv.QUOTE_ALL)
+        w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "Percentage", "MinNs", "MaxNs"])
+        tot = sum(sum(v) for v in per.values())
+        for name, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+            w.writerow([name, len(v), sum(v), "%.1f" % (sum(v) / len(v)), "%.2f" % (100.0 * sum(v) / tot),
+                        min(v), max(v)])
+            rows.append((short(name), len(v), sum(v) / len(v)))
+    for r in rows:
+        print("%-28s %4d launches  avg %10.1f us" % (r[0], r[1], r[2] / 1e3))
+
+# ---- PMC passes
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
-    path = os.path.join(src, sub, "p_counter_collection.csv")
-    if not os.path.exists(path):
+    db = one_db(sub + "/*results.db")
+    if db is None:
         continue
-    for r in csv.DictReader(open(path)):
-        agg[r["Kernel_Name"].split("(")[0].replace("bn::", "")][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    # counters_collection holds one row per (dispatch, counter), already summed over instances
+    for kname, cname, val in db.execute("select kernel_name, counter_name, value from counters_collection"):
+        agg[short(kname)][cname].append(float(val))
 summary = {}
-lines = ["%-16s %14s %14s %14s %12s %10s" % ("kernel", "FETCH_bytes", "WRITE_bytes", "VALU/wave", "WAVE_CYC/w", "VALU/cyc")]
+lines = ["%-16s %14s %14s %14s %12s %10s" % ("kernel", "FETCH_bytes", "WRITE_bytes", "VALU/wave", "WAVE_CYC/w",
+                                                 "VALU/cyc")]
 for k, v in sorted(agg.items()):
     if k.startswith("__amd"):
         continue
@@ -30,12 +74,15 @@ for k, v in sorted(agg.items()):
     write = m.get("WRITE_SIZE", 0) * 1024
     waves = m.get("SQ_WAVES", 0) or 1
     valu = m.get("SQ_INSTS_VALU", 0) / waves
-    cyc = m.get("SQ_WAVE_CYCLES", 0) * 4 / waves  # quad-cycles
+    cyc = m.get("SQ_WAVE_CYCLES", 0) * 4 / waves  # quad-cycles -> cycles
     summary[k] = {"hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
                   "valu_insts_per_wave": valu, "wave_cycles": cyc,
                   "valu_per_cycle_per_wave": valu / cyc if cyc else None,
-                  "note": "FETCH_SIZE/WRITE_SIZE raw (KiB*1024); dword loads uncalibrated (MI355X_MICROARCH §HBM)"}
+                  "grbm_gui_active": m.get("GRBM_GUI_ACTIVE"),
+                  "note": "FETCH_SIZE/WRITE_SIZE raw (KiB*1024); 4-B/lane dword accesses are uncalibrated "
+                          "(MI355X_MICROARCH §HBM); source %s" % tag}
     lines.append("%-16s %14.3e %14.3e %14.3e %12.3e %10.3f" % (k, fetch, write, valu, cyc, valu / cyc if cyc else 0))
-json.dump(summary, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
-open(os.path.join(out_dir, "%s_pmc.txt" % tag), "w").write("\n".join(lines) + "\n")
-print("\n".join(lines))
+if summary:
+    json.dump(summary, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
+    open(os.path.join(out_dir, "%s_pmc.txt" % tag), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
