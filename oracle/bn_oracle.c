@@ -916,3 +916,314 @@ static void run_many(int kind, const void* a, const void* b, size_t n, void* out
 void orc_pairing_many(const orc_g1* p, const orc_g2* q, size_t n, orc_fq12* out, int nthreads) { run_many(0, p, q, n, out, nthreads); }
 void orc_g1_mul_many(const orc_g1* p, const orc_fe* k, size_t n, orc_g1* out, int nthreads) { run_many(1, p, k, n, out, nthreads); }
 void orc_g2_mul_many(const orc_g2* p, const orc_fe* k, size_t n, orc_g2* out, int nthreads) { run_many(2, p, k, n, out, nthreads); }
+
+/* ------------------------------------------------------------------ */
+/* Encodings, validation, square roots, decompression, Gt::pow        */
+/*                                          */
+
+/* U256::from_slice, arith.rs:202-216 (32 bytes big endian; the length check is the caller's) */
+static u256 u256_from_be(const uint8_t* s) {
+    u256 r;
+    for (int l = 1, i = 0; l >= 0; --l, i += 16) {
+        u128 v = 0;
+        for (int k = 0; k < 16; ++k) v = (v << 8) | s[i + k];           /* BigEndian::read_u128 */
+        r.d[l] = v;
+    }
+    return r;
+}
+/* U256::to_big_endian, arith.rs:218-231 */
+static void u256_to_be(u256 a, uint8_t* s) {
+    for (int l = 1, i = 0; l >= 0; --l, i += 16)
+        for (int k = 0; k < 16; ++k) s[i + k] = (uint8_t)(a.d[l] >> (8 * (15 - k)));
+}
+typedef struct { u128 d[4]; } u512;                                  /* arith.rs:23 */
+static u512 u512_from_be(const uint8_t* s) {                        /* arith.rs:82-96 */
+    u512 r;
+    for (int l = 3, i = 0; l >= 0; --l, i += 16) {
+        u128 v = 0;
+        for (int k = 0; k < 16; ++k) v = (v << 8) | s[i + k];
+        r.d[l] = v;
+    }
+    return r;
+}
+static int u256_set_bit(u256* a, int n, int to) {                  /* arith.rs:252-267 */
+    if (n >= 256) return 0;
+    const int part = n / 128, bit = n - 128 * part;
+    if (to) a->d[part] |= (u128)1 << bit; else a->d[part] &= ~((u128)1 << bit);
+    return 1;
+}
+/* U512::divrem, arith.rs:116-138: remainder, and the quotient if it is below the modulus */
+static int u512_divrem(const u512* a, const u256* m, u256* q_out, u256* r_out) {
+    int q_some = 1;
+    u256 q = U(0, 0, 0, 0), r = U(0, 0, 0, 0);
+    for (int i = 511; i >= 0; --i) {
+        const u128 top = r.d[0] >> 127;                              /* mul2, arith.rs:409-414 */
+        r.d[0] <<= 1;
+        r.d[1] = (r.d[1] << 1) | top;
+        u256_set_bit(&r, 0, (int)((a->d[i / 128] >> (i % 128)) & 1));
+        if (u256_cmp(&r, m) >= 0) {
+            sub_noborrow(r.d, m->d);
+            if (q_some && !u256_set_bit(&q, i, 1)) q_some = 0;
+        }
+    }
+    if (q_some && u256_cmp(&q, m) >= 0) q_some = 0;
+    *q_out = q;
+    *r_out = r;
+    return q_some;
+}
+/* U512::new(c1, c0, modulo) = c1 * modulo + c0, arith.rs:47-80 (used by Fq2::to_u512) */
+static u512 u512_new(const u256* c1, const u256* c0, const u256* m) {
+    u128 res[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 2; ++i) mac_digit(i, res, m->d, c1->d[i]);
+    u128 carry = 0;
+    for (int i = 0; i < 2; ++i) res[i] = adc(res[i], c0->d[i], &carry);
+    for (int i = 0; i < 2; ++i) {
+        const u128 a1 = res[i + 2] >> 64, a0 = res[i + 2] & M64;
+        u128 s0 = a0 + carry, c = s0 >> 64, r0 = s0 & M64;
+        u128 s1 = a1 + c, r1 = s1 & M64;
+        carry = s1 >> 64;
+        res[i + 2] = (r1 << 64) | r0;
+    }
+    u512 o = {{res[0], res[1], res[2], res[3]}};
+    return o;
+}
+static int u512_cmp(const u512* a, const u512* b) {                 /* arith.rs:147-160 */
+    for (int i = 3; i >= 0; --i) {
+        if (a->d[i] < b->d[i]) return -1;
+        if (a->d[i] > b->d[i]) return 1;
+    }
+    return 0;
+}
+
+/* Fp::new (fp.rs:46-54): below the modulus -> Montgomery, else None */
+static int fe_new(u256 a, const fparams* P, fe* out) {
+    if (u256_cmp(&a, &P->m) >= 0) return 1;
+    u256_mul(&a, &P->r2, &P->m, P->inv);
+    *out = a;
+    return 0;
+}
+static u256 fe_into_u256(fe a, const fparams* P) {                 /* fp.rs:13-20 */
+    u256 one = U(1, 0, 0, 0);
+    u256_mul(&a, &one, &P->m, P->inv);
+    return a;
+}
+/* generic FieldElement::pow, fields/mod.rs:35-46 (256 bits, MSB first) */
+static fe fe_pow(fe a, u256 by, const fparams* P) {
+    fe res = P->one;
+    for (int n = 255; n >= 0; --n) {
+        res = fe_squared(res, P);
+        if ((by.d[n / 128] >> (n % 128)) & 1) res = fe_mul(a, res, P);
+    }
+    return res;
+}
+static fq2 fq2_pow(fq2 a, u256 by) {
+    fq2 res = fq2_one();
+    for (int n = 255; n >= 0; --n) {
+        res = fq2_squared(res);
+        if ((by.d[n / 128] >> (n % 128)) & 1) res = fq2_mul(a, res);
+    }
+    return res;
+}
+/* lazy_static FQ_MINUS3_DIV4 / FQ_MINUS1_DIV2 (fp.rs:235-243, fq2.rs:192-200), as U256 (canonical) */
+static u256 fq_minus3_div4(void) {
+    fe three, four, inv4;
+    fe_new(U(3, 0, 0, 0), FQ, &three);
+    fe_new(U(4, 0, 0, 0), FQ, &four);
+    inv4 = four;
+    fe_inverse(&inv4, FQ);
+    return fe_into_u256(fe_mul(fe_neg(three, FQ), inv4, FQ), FQ);
+}
+static u256 fq_minus1_div2(void) {
+    fe one, two, inv2;
+    fe_new(U(1, 0, 0, 0), FQ, &one);
+    fe_new(U(2, 0, 0, 0), FQ, &two);
+    inv2 = two;
+    fe_inverse(&inv2, FQ);
+    return fe_into_u256(fe_mul(fe_neg(one, FQ), inv2, FQ), FQ);
+}
+/* Fq::sqrt, fp.rs:245-260 */
+static int fq_sqrt(fe a, fe* out) {
+    fe a1 = fe_pow(a, fq_minus3_div4(), FQ);
+    fe a1a = fq_mul(a1, a);
+    fe a0 = fq_mul(a1, a1a);
+    u256 am1 = FQ->m;
+    u256 one = U(1, 0, 0, 0);
+    u256_sub(&am1, &one, &FQ->m);
+    fe m1;
+    fe_new(am1, FQ, &m1);
+    if (fq_eq(a0, m1)) return 1;
+    *out = a1a;
+    return 0;
+}
+static fq2 fq2_i(void) { return F2(fq_zero(), fq_one()); }       /* fq2.rs:203-205 */
+/* Fq2::sqrt, fq2.rs:208-224 */
+static int fq2_sqrt(fq2 a, fq2* out) {
+    fq2 a1 = fq2_pow(a, fq_minus3_div4());
+    fq2 a1a = fq2_mul(a1, a);
+    fq2 alpha = fq2_mul(a1, a1a);
+    fq2 a0 = fq2_mul(fq2_pow(alpha, FQ->m), alpha);
+    const fq2 neg_one = fq2_neg(fq2_one());
+    if (fq2_eq(a0, neg_one)) return 1;
+    if (fq2_eq(alpha, neg_one)) {
+        *out = fq2_mul(fq2_i(), a1a);
+    } else {
+        fq2 b = fq2_pow(fq2_add(alpha, fq2_one()), fq_minus1_div2());
+        *out = fq2_mul(b, a1a);
+    }
+    return 0;
+}
+static u512 fq2_to_u512(fq2 a) {                                   /* fq2.rs:226-231 */
+    u256 c0 = fe_into_u256(a.c0, FQ), c1 = fe_into_u256(a.c1, FQ);
+    return u512_new(&c1, &c0, &FQ->m);
+}
+
+/* AffineG::new, mod.rs:95-113 (G1: check_order false; G2: true) */
+static int g1_affine_new(fe x, fe y) {
+    if (!fq_eq(fq_sq(y), fq_add(fq_mul(fq_sq(x), x), g1_coeff_b()))) return ORC_GROUP_NOT_ON_CURVE;
+    return ORC_OK;
+}
+static int g2_affine_new(fq2 x, fq2 y) {
+    if (!fq2_eq(fq2_squared(y), fq2_add(fq2_mul(fq2_squared(x), x), g2_coeff_b()))) return ORC_GROUP_NOT_ON_CURVE;
+    g2 p = {x, y, fq2_one()};
+    /* p * (-Fr::one()) + p != G::zero(); U256::from(-Fr::one()) = r - 1 */
+    u256 rm1 = FRP.m;
+    rm1.d[0] -= 1;                                                   /* r is odd: no borrow */
+    g2 t = g2_mul_u256(&p, rm1);
+    t = g2_add(&t, &p);
+    g2 z = g2_zero();
+    if (!g2_eq(&t, &z)) return ORC_GROUP_NOT_IN_SUBGROUP;
+    return ORC_OK;
+}
+
+/* ---- exported ---- */
+int orc_fq_from_slice(const uint8_t* s, orc_fe* out) {             /* lib.rs:154-159 */
+    FP(0);
+    fe x;
+    if (fe_new(u256_from_be(s), FQ, &x)) return ORC_FIELD_NOT_MEMBER;
+    ST(fe, out, x);
+    return ORC_OK;
+}
+void orc_fq_to_big_endian(const orc_fe* a, uint8_t* s) {            /* lib.rs:160-170 */
+    FP(0);
+    u256 x = fe_into_u256(LD(fe, a), FQ);
+    u256_mul(&x, &FQ->one, &FQ->m, FQ->inv);
+    u256_to_be(x, s);
+}
+int orc_fq2_from_slice(const uint8_t* s, orc_fq2* out) {           /* lib.rs:260-267 */
+    FP(0);
+    u512 v = u512_from_be(s);
+    u256 q, r;
+    int q_some = u512_divrem(&v, &FQ->m, &q, &r);
+    fe c0, c1;
+    if (fe_new(r, FQ, &c0)) return ORC_FIELD_NOT_MEMBER;
+    if (!q_some) return ORC_FIELD_NOT_MEMBER;
+    if (fe_new(q, FQ, &c1)) return ORC_FIELD_NOT_MEMBER;
+    fq2 o = F2(c0, c1);
+    ST(fq2, out, o);
+    return ORC_OK;
+}
+void orc_fr_from_slice(const uint8_t* s, orc_fe* out) {             /* lib.rs:45-49, fp.rs:57-60 */
+    u256 a = u256_from_be(s);
+    const fparams* P = FP(1);
+    u256_mul(&a, &P->r2, &P->m, P->inv);                             /* new_mul_factor */
+    ST(fe, out, a);
+}
+void orc_fr_to_big_endian(const orc_fe* a, uint8_t* s) {            /* lib.rs:50-55: raw Montgomery */
+    u256_to_be(LD(u256, a), s);
+}
+int orc_u512_divrem(const uint8_t* be64, orc_fe* q, orc_fe* r) {    /* arith.rs:116-138; 1 = quotient Some */
+    FP(0);
+    u512 v = u512_from_be(be64);
+    return u512_divrem(&v, &FQ->m, (u256*)(void*)q, (u256*)(void*)r);
+}
+int orc_fq_sqrt(const orc_fe* a, orc_fe* out) { FP(0); return fq_sqrt(LD(fe, a), (fe*)(void*)out); }
+int orc_fq2_sqrt(const orc_fq2* a, orc_fq2* out) { FP(0); return fq2_sqrt(LD(fq2, a), (fq2*)(void*)out); }
+int orc_g1_affine_new(const orc_fe* x, const orc_fe* y, orc_g1* out) {
+    FP(0);
+    int st = g1_affine_new(LD(fe, x), LD(fe, y));
+    if (st == ORC_OK) { g1 p = {LD(fe, x), LD(fe, y), fq_one()}; ST(g1, out, p); }  /* to_jacobian, mod.rs:220-226 */
+    return st;
+}
+int orc_g2_affine_new(const orc_fq2* x, const orc_fq2* y, orc_g2* out) {
+    FP(0);
+    int st = g2_affine_new(LD(fq2, x), LD(fq2, y));
+    if (st == ORC_OK) { g2 p = {LD(fq2, x), LD(fq2, y), fq2_one()}; ST(g2, out, p); }
+    return st;
+}
+/* G1::from_compressed, lib.rs:359-375 */
+int orc_g1_from_compressed(const uint8_t* bytes, size_t len, orc_g1* out) {
+    FP(0);
+    if (len != 33) return ORC_CURVE_INVALID_ENCODING;
+    const uint8_t sign = bytes[0];
+    fe x;
+    if (fe_new(u256_from_be(bytes + 1), FQ, &x)) return ORC_FIELD_NOT_MEMBER;  /* CurveError::Field(NotMember) */
+    fe y_squared = fq_add(fq_mul(fq_mul(x, x), x), g1_coeff_b());
+    fe y;
+    if (fq_sqrt(y_squared, &y)) return ORC_CURVE_NOT_MEMBER;
+    const int odd = (int)(fe_into_u256(y, FQ).d[0] & 1);
+    if (sign == 2 && odd) y = fq_neg(y);
+    else if (sign == 3 && !odd) y = fq_neg(y);
+    else if (sign != 3 && sign != 2) return ORC_CURVE_INVALID_ENCODING;
+    if (g1_affine_new(x, y) != ORC_OK) return ORC_CURVE_NOT_MEMBER;
+    g1 p = {x, y, fq_one()};
+    ST(g1, out, p);
+    return ORC_OK;
+}
+/* G2::from_compressed, lib.rs:506-526 */
+int orc_g2_from_compressed(const uint8_t* bytes, size_t len, orc_g2* out) {
+    FP(0);
+    if (len != 65) return ORC_CURVE_INVALID_ENCODING;
+    const uint8_t sign = bytes[0];
+    fq2 x;
+    int st = orc_fq2_from_slice(bytes + 1, (orc_fq2*)(void*)&x);
+    if (st != ORC_OK) return st;                                     /* CurveError::Field(..) */
+    fq2 y_squared = fq2_add(fq2_mul(fq2_mul(x, x), x), g2_coeff_b());
+    fq2 y;
+    if (fq2_sqrt(y_squared, &y)) return ORC_CURVE_NOT_MEMBER;
+    fq2 y_neg = fq2_neg(y);
+    u512 a = fq2_to_u512(y), b = fq2_to_u512(y_neg);
+    const int y_gt = u512_cmp(&a, &b) > 0;
+    fq2 e_y;
+    if (sign == 10) e_y = y_gt ? y_neg : y;
+    else if (sign == 11) e_y = y_gt ? y : y_neg;
+    else return ORC_CURVE_INVALID_ENCODING;
+    if (g2_affine_new(x, e_y) != ORC_OK) return ORC_CURVE_NOT_MEMBER;
+    g2 p = {x, e_y, fq2_one()};
+    ST(g2, out, p);
+    return ORC_OK;
+}
+/* Gt::pow, lib.rs:592-594 -> Fq12 pow (fields/mod.rs:35-46) by U256::from(Fr) */
+void orc_gt_pow(const orc_fq12* a, const orc_fe* fr_mont, orc_fq12* out) {
+    FP(0);
+    u256 e = fe_into_u256(LD(fe, fr_mont), FP(1));
+    ST(fq12, out, fq12_pow(LD(fq12, a), e));
+}
+
+/* threaded forms for the large-sample parity tests */
+typedef struct { int kind; const uint8_t* in; void* out; uint8_t* st; size_t lo, hi; } cjob;
+static void* run_cjob(void* arg) {
+    cjob* j = (cjob*)arg;
+    for (size_t i = j->lo; i < j->hi; ++i) {
+        if (j->kind == 0) j->st[i] = (uint8_t)orc_g1_from_compressed(j->in + 33 * i, 33, (orc_g1*)j->out + i);
+        else if (j->kind == 1) j->st[i] = (uint8_t)orc_g2_from_compressed(j->in + 65 * i, 65, (orc_g2*)j->out + i);
+        else {
+            const orc_fq2* xy = (const orc_fq2*)(const void*)j->in + 2 * i;
+            j->st[i] = (uint8_t)orc_g2_affine_new(&xy[0], &xy[1], (orc_g2*)j->out + i);
+        }
+    }
+    return NULL;
+}
+void orc_decode_many(int kind, const uint8_t* in, size_t n, void* out, uint8_t* status, int nthreads) {
+    FP(0);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((size_t)nthreads > n) nthreads = n ? (int)n : 1;
+    pthread_t th[256];
+    cjob jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        cjob j = {kind, in, out, status, n * t / nthreads, n * (t + 1) / nthreads};
+        jobs[t] = j;
+        pthread_create(&th[t], NULL, run_cjob, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}

@@ -95,6 +95,35 @@ void orc_pairing_many(const orc_g1* p, const orc_g2* q, size_t n, orc_fq12* out,
 void orc_g1_mul_many(const orc_g1* p, const orc_fe* k, size_t n, orc_g1* out, int nthreads);
 void orc_g2_mul_many(const orc_g2* p, const orc_fe* k, size_t n, orc_g2* out, int nthreads);
 
+
+/* ---- encodings / validation / decompression / Gt::pow ----
+ * per-element status, same values as bn_elem_status in include/bn254mi.h */
+enum {
+    ORC_OK = 0,
+    ORC_FIELD_INVALID_SLICE_LENGTH = 1, /* FieldError::InvalidSliceLength (lib.rs:99-104) */
+    ORC_FIELD_INVALID_U512 = 2,         /* FieldError::InvalidU512Encoding */
+    ORC_FIELD_NOT_MEMBER = 3,           /* FieldError::NotMember */
+    ORC_CURVE_INVALID_ENCODING = 4,     /* CurveError::InvalidEncoding (lib.rs:106-112) */
+    ORC_CURVE_NOT_MEMBER = 5,           /* CurveError::NotMember */
+    ORC_GROUP_NOT_ON_CURVE = 6,         /* groups::Error::NotOnCurve (mod.rs:89-92) */
+    ORC_GROUP_NOT_IN_SUBGROUP = 7       /* groups::Error::NotInSubgroup */
+};
+int  orc_fq_from_slice(const uint8_t* be32, orc_fe* out);
+void orc_fq_to_big_endian(const orc_fe* a, uint8_t* be32);
+int  orc_fq2_from_slice(const uint8_t* be64, orc_fq2* out);
+void orc_fr_from_slice(const uint8_t* be32, orc_fe* out);
+void orc_fr_to_big_endian(const orc_fe* a, uint8_t* be32);
+int  orc_u512_divrem(const uint8_t* be64, orc_fe* q, orc_fe* r);
+int  orc_fq_sqrt(const orc_fe* a, orc_fe* out);                   /* 0 Some, 1 None */
+int  orc_fq2_sqrt(const orc_fq2* a, orc_fq2* out);
+int  orc_g1_affine_new(const orc_fe* x, const orc_fe* y, orc_g1* out);
+int  orc_g2_affine_new(const orc_fq2* x, const orc_fq2* y, orc_g2* out);
+int  orc_g1_from_compressed(const uint8_t* bytes, size_t len, orc_g1* out);
+int  orc_g2_from_compressed(const uint8_t* bytes, size_t len, orc_g2* out);
+void orc_gt_pow(const orc_fq12* a, const orc_fe* fr_mont, orc_fq12* out);
+/* kind 0: G1 compressed (33 B), 1: G2 compressed (65 B), 2: G2 affine (x, y) validation */
+void orc_decode_many(int kind, const uint8_t* in, size_t n, void* out, uint8_t* status, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

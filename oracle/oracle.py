@@ -130,6 +130,20 @@ def lib():
             "orc_pairing_many": ([vp, vp, sz, vp, i], None),
             "orc_g1_mul_many": ([vp, vp, sz, vp, i], None),
             "orc_g2_mul_many": ([vp, vp, sz, vp, i], None),
+            "orc_fq_from_slice": ([vp, vp], i),
+            "orc_fq_to_big_endian": ([vp, vp], None),
+            "orc_fq2_from_slice": ([vp, vp], i),
+            "orc_fr_from_slice": ([vp, vp], None),
+            "orc_fr_to_big_endian": ([vp, vp], None),
+            "orc_u512_divrem": ([vp, vp, vp], i),
+            "orc_fq_sqrt": ([vp, vp], i),
+            "orc_fq2_sqrt": ([vp, vp], i),
+            "orc_g1_affine_new": ([vp, vp, vp], i),
+            "orc_g2_affine_new": ([vp, vp, vp], i),
+            "orc_g1_from_compressed": ([vp, sz, vp], i),
+            "orc_g2_from_compressed": ([vp, sz, vp], i),
+            "orc_gt_pow": ([vp, vp, vp], None),
+            "orc_decode_many": ([i, vp, sz, vp, vp, i], None),
         }
         for name, (args, res) in sigs.items():
             fn = getattr(L, name)
@@ -284,6 +298,122 @@ def g1_eq(a, b):
 def g2_eq(a, b):
     a, b = _u64(a, 24), _u64(b, 24)
     return [bool(lib().orc_g2_eq(_p(a[k]), _p(b[k]))) for k in range(a.shape[0])]
+
+
+# ---------------------------------------------------------------- encodings
+# per-element status codes (bn_oracle.h ORC_*, == bn_elem_status of include/bn254mi.h)
+OK, FIELD_INVALID_SLICE_LENGTH, FIELD_INVALID_U512, FIELD_NOT_MEMBER = 0, 1, 2, 3
+CURVE_INVALID_ENCODING, CURVE_NOT_MEMBER, GROUP_NOT_ON_CURVE, GROUP_NOT_IN_SUBGROUP = 4, 5, 6, 7
+
+
+def _u8(a, width):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    assert a.size % width == 0, (a.shape, width)
+    return a.reshape(-1, width)
+
+
+def _rows(fn, inp, win, wout, dtype_out=np.uint64, has_status=True):
+    """apply fn(in_row, out_row) -> status to every row."""
+    out = np.zeros((inp.shape[0], wout), dtype=dtype_out)
+    st = np.zeros(inp.shape[0], dtype=np.uint8)
+    for k in range(inp.shape[0]):
+        rc = fn(_p(inp[k]), _p(out[k]))
+        if has_status:
+            st[k] = rc
+    return out, st
+
+
+def fq_from_slice(be):
+    return _rows(lib().orc_fq_from_slice, _u8(be, 32), 32, 4)
+
+
+def fq_to_big_endian(a):
+    return _rows(lib().orc_fq_to_big_endian, _u64(a, 4), 4, 32, np.uint8, False)[0]
+
+
+def fq2_from_slice(be):
+    return _rows(lib().orc_fq2_from_slice, _u8(be, 64), 64, 8)
+
+
+def fr_from_slice(be):
+    return _rows(lib().orc_fr_from_slice, _u8(be, 32), 32, 4, has_status=False)[0]
+
+
+def fr_to_big_endian(a):
+    return _rows(lib().orc_fr_to_big_endian, _u64(a, 4), 4, 32, np.uint8, False)[0]
+
+
+def u512_divrem(be64):
+    """(q, r, q_is_some) of U512::divrem by the Fq modulus, plain integers."""
+    b = _u8(be64, 64)[0]
+    q = np.zeros(4, dtype=np.uint64)
+    r = np.zeros(4, dtype=np.uint64)
+    some = lib().orc_u512_divrem(_p(b), _p(q), _p(r))
+    return limbs_to_int(q), limbs_to_int(r), bool(some)
+
+
+def fq_sqrt(a):
+    out, st = _rows(lib().orc_fq_sqrt, _u64(a, 4), 4, 4)
+    return out, st == 0
+
+
+def fq2_sqrt(a):
+    out, st = _rows(lib().orc_fq2_sqrt, _u64(a, 8), 8, 8)
+    return out, st == 0
+
+
+def g1_affine_new(x, y):
+    x, y = _u64(x, 4), _u64(y, 4)
+    out = np.zeros((x.shape[0], 12), dtype=np.uint64)
+    st = np.array([lib().orc_g1_affine_new(_p(x[k]), _p(y[k]), _p(out[k])) for k in range(x.shape[0])], np.uint8)
+    return out, st
+
+
+def g2_affine_new(x, y, nthreads=1):
+    x, y = _u64(x, 8), _u64(y, 8)
+    xy = np.ascontiguousarray(np.concatenate([x, y], axis=1))
+    n = x.shape[0]
+    out = np.zeros((n, 24), dtype=np.uint64)
+    st = np.zeros(n, dtype=np.uint8)
+    lib().orc_decode_many(2, _p(xy), n, _p(out), _p(st), nthreads)
+    return out, st
+
+
+def g1_from_compressed(b, nthreads=1):
+    b = _u8(b, 33)
+    n = b.shape[0]
+    out = np.zeros((n, 12), dtype=np.uint64)
+    st = np.zeros(n, dtype=np.uint8)
+    lib().orc_decode_many(0, _p(b), n, _p(out), _p(st), nthreads)
+    return out, st
+
+
+def g2_from_compressed(b, nthreads=1):
+    b = _u8(b, 65)
+    n = b.shape[0]
+    out = np.zeros((n, 24), dtype=np.uint64)
+    st = np.zeros(n, dtype=np.uint8)
+    lib().orc_decode_many(1, _p(b), n, _p(out), _p(st), nthreads)
+    return out, st
+
+
+def g1_from_compressed_one(b):
+    """G1::from_compressed on one slice of any length (length errors included)."""
+    buf = np.frombuffer(bytes(b) + b"\0", dtype=np.uint8).copy()
+    out = np.zeros(12, dtype=np.uint64)
+    st = lib().orc_g1_from_compressed(_p(buf), len(b), _p(out))
+    return out, st
+
+
+def g2_from_compressed_one(b):
+    buf = np.frombuffer(bytes(b) + b"\0", dtype=np.uint8).copy()
+    out = np.zeros(24, dtype=np.uint64)
+    st = lib().orc_g2_from_compressed(_p(buf), len(b), _p(out))
+    return out, st
+
+
+def gt_pow(a, k):
+    return binary("orc_gt_pow", a, k, 48, 4, 48)
 
 
 # ---------------------------------------------------------------- seeded inputs

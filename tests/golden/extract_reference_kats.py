@@ -15,6 +15,12 @@ Sources (file:line in /root/reference):
   fq12_test_vector      src/fields/mod.rs:94-227
   test_cyclotomic_exp   src/fields/mod.rs:230-344
   test_str              src/fields/mod.rs:68-81
+  sqrt_fq               src/fields/fp.rs:289-296
+  sqrt_fq2              src/fields/fq2.rs:235-258
+  g1_from_compressed    src/lib.rs:681-689
+  g2_from_compressed    src/lib.rs:691-743
+  testing_divrem        src/arith.rs:588-666 (the two fixed U512 cases)
+  from_slice / to_big_endian  src/arith.rs:561-586
 """
 import json
 import os
@@ -91,6 +97,51 @@ def main():
     s = strs(body)
     assert len(s) == 2
     kats["test_str"] = {"where": "src/fields/mod.rs:%d" % line, "fr_minus_one": s[0], "fq_minus_one": s[1]}
+
+    fp = open(os.path.join(REF, "fields/fp.rs")).read()
+    body, line = fn_body(fp, "sqrt_fq")
+    s = strs(body)
+    assert len(s) == 2
+    kats["sqrt_fq"] = {"where": "src/fields/fp.rs:%d" % line, "root": s[0], "square": s[1]}
+
+    fq2 = open(os.path.join(REF, "fields/fq2.rs")).read()
+    body, line = fn_body(fq2, "sqrt_fq2")
+    s = strs(body)
+    assert len(s) == 6, s
+    kats["sqrt_fq2"] = {"where": "src/fields/fq2.rs:%d" % line, "root": s[0:2], "square": s[2:4],
+                        "minus_one_root": "i = (0, 1)", "no_root": s[4:6]}
+
+    lib = open(os.path.join(REF, "lib.rs")).read()
+    hex_re = re.compile(r'hex\("([0-9a-f]+)"\)')
+    i1, i2 = lib.index("fn g1_from_compressed"), lib.index("fn g2_from_compressed")
+    body, line = lib[i1:i2], lib[:i1].count("\n") + 1
+    h, s = hex_re.findall(body), strs(body)
+    assert len(h) == 1 and len(s) == 2
+    kats["g1_from_compressed"] = {"where": "src/lib.rs:%d" % line, "bytes": h[0], "x": s[0], "y": s[1]}
+    body, line = lib[i2:], lib[:i2].count("\n") + 1
+    h, s = hex_re.findall(body), strs(body)
+    assert len(h) == 3 and len(s) == 8 and s[4:8] == s[0:4], (len(h), len(s))
+    kats["g2_from_compressed"] = {"where": "src/lib.rs:%d" % line, "bytes_0a": h[0], "bytes_0b_negated": h[1],
+                                  "bytes_0c_invalid": h[2], "x": s[0:2], "y": s[2:4]}
+
+    arith = open(os.path.join(REF, "arith.rs")).read()
+    body, line = fn_body(arith, "testing_divrem")
+    arr = re.findall(r"from\(\[([^\]]*)\]\)", body)
+    words = [[int(w.strip(), 16) for w in a.split(",") if w.strip()] for a in arr]
+    big = lambda ws: str(sum(w << (64 * i) for i, w in enumerate(ws)))
+    # blocks in order: Fq modulus; p -> (1, 0); p^2-1 -> (q, r); p^2-2 -> (q, r);
+    # "ridiculously large" -> (None, r); p^2 -> (None, 0); p^2+1 -> (None, 1);
+    # Fr modulus, then "Fr modulus masked off" -> (Some(q < r), r' < r)
+    assert [len(w) for w in words] == [4, 8, 8, 4, 4, 8, 4, 4, 8, 4, 8, 8, 4, 8], [len(w) for w in words]
+    cases = [{"a": big(words[1]), "q": "1", "r": "0"},
+             {"a": big(words[2]), "q": big(words[3]), "r": big(words[4])},
+             {"a": big(words[5]), "q": big(words[6]), "r": big(words[7])},
+             {"a": big(words[8]), "q": None, "r": big(words[9])},
+             {"a": big(words[10]), "q": None, "r": "0"},
+             {"a": big(words[11]), "q": None, "r": "1"}]
+    kats["testing_divrem"] = {"where": "src/arith.rs:%d" % line, "modulo": big(words[0]), "cases": cases,
+                              "fr_modulo": big(words[12]), "fr_masked_a": big(words[13])}
+    kats["u256_one_big_endian"] = {"where": "src/arith.rs:561-586", "bytes": "00" * 31 + "01", "value": "1"}
 
     with open(OUT, "w") as fh:
         json.dump(kats, fh, indent=1)
