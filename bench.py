@@ -137,6 +137,84 @@ def other_workload(args, local_rank):
     print(json.dumps(res), flush=True)
 
 
+def codec_workload(args, local_rank):
+    """SURVEY 8(f) rows on 2^16 elements, inputs resident in HBM, device-pointer C ABI on torch's stream."""
+    import torch
+
+    from oracle import oracle as O
+    from substrate_bn import Context
+    from tests.codec_util import compress_g2
+
+    dev = torch.device("cuda", local_rank)
+    ctx = Context(local_rank)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    n = args.pairs
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    if args.workload in ("g2validate", "g2decompress"):
+        _, t = O.random_scalars(n, 61)
+        aff, _ = O.g2_to_affine(O.g2_mul(O.g2_one(), t, threads))  # n distinct points of the order-r subgroup
+        out = torch.empty((n, 24), dtype=torch.int64, device=dev)
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        if args.workload == "g2validate":
+            x = torch.from_numpy(np.ascontiguousarray(aff[:, :8]).view(np.int64)).to(dev)
+            y = torch.from_numpy(np.ascontiguousarray(aff[:, 8:]).view(np.int64)).to(dev)
+            step = lambda: ctx.g2_affine_new_many_dev(x.data_ptr(), y.data_ptr(), n, out.data_ptr(),  # noqa: E731
+                                                      st.data_ptr(), sh)
+            unit, kname = "G2 validations/s", "k_g2_affine_new"
+            wl = "AffineG2::new on 2^16 affine points (curve equation + order check [r]P == 0), mod.rs:95-113"
+            ref_fn = lambda m: O.g2_affine_new(aff[:m, :8], aff[:m, 8:], threads)  # noqa: E731
+        else:
+            rec = compress_g2(aff)
+            b = torch.from_numpy(rec).to(dev)
+            step = lambda: ctx.g2_from_compressed_many_dev(b.data_ptr(), n, out.data_ptr(), st.data_ptr(), sh)  # noqa
+            unit, kname = "G2 decompressions/s", "k_g2_from_compressed"
+            wl = "G2::from_compressed on 2^16 65-byte records (Fq2 sqrt + order check), lib.rs:506-526"
+            ref_fn = lambda m: O.g2_from_compressed(rec[:m], threads)  # noqa: E731
+    else:
+        p, q, _, _ = O.random_pairs(1024, seed=71, nthreads=threads)
+        g = O.pairing_many(p, q, threads)
+        a = torch.from_numpy(np.ascontiguousarray(np.tile(g, (n // 1024, 1))).view(np.int64)).to(dev)
+        _, k = O.random_scalars(n, 72, lo=0)
+        kt = torch.from_numpy(np.ascontiguousarray(k).view(np.int64)).to(dev)
+        out = torch.empty((n, 48), dtype=torch.int64, device=dev)
+        st = None
+        step = lambda: ctx.gt_pow_many_dev(a.data_ptr(), kt.data_ptr(), n, out.data_ptr(), sh)  # noqa: E731
+        unit, kname = "Gt pows/s", "k_gt_pow"
+        wl = "Gt::pow(Fr) on 2^16 (Gt, uniform Fr) pairs (1024 distinct pairing outputs tiled), lib.rs:592-594"
+        a_h = np.ascontiguousarray(np.tile(g, (n // 1024, 1)))
+        ref_fn = lambda m: (O.gt_pow(a_h[:m], k[:m]), None)  # noqa: E731
+    log("inputs ready in %.1f s" % (time.perf_counter() - t0))
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    kms = e0.elapsed_time(e1) / args.steps
+    res = {"metric": unit, "value": n * args.steps / el, "unit": unit, "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)", "data": "synthetic",
+           "config": {"workload": wl, "elements": n},
+           "kernel": {"name": kname, "per_launch_ms": kms}}
+    m = min(args.cpu_sample, n)
+    g_out = out[:m].cpu().numpy().view(np.uint64)
+    t0 = time.perf_counter()
+    ref, rst = ref_fn(m)
+    dt = time.perf_counter() - t0
+    same = np.array_equal(ref, g_out) and (rst is None or np.array_equal(rst, st[:m].cpu().numpy()))
+    res["cpu_baseline"] = {"value": m / dt, "unit": unit, "cores": threads, "kind": "port",
+                           "sample": "%d elements of the bench inputs, oracle, %d threads" % (m, threads),
+                           "parity_sample_bit_exact": bool(same)}
+    print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,9 +223,11 @@ def main():
     ap.add_argument("--pairs", type=int, default=1 << 16, help="pairings per GPU per step")
     ap.add_argument("--cpu-sample", type=int, default=2048)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", default="pairing", choices=["pairing", "g1mul", "product"],
+    ap.add_argument("--workload", default="pairing",
+                    choices=["pairing", "g1mul", "product", "g2validate", "g2decompress", "gtpow"],
                     help="pairing: config 2 (default); g1mul: config 3 (2^18 G1*Fr); product: config 5 "
-                         "(2^14-term pairing_batch)")
+                         "(2^14-term pairing_batch); SURVEY 8(f): g2validate (AffineG2::new incl. the order "
+                         "check), g2decompress (G2::from_compressed), gtpow (Gt::pow(Fr)), 2^16 each")
     args = ap.parse_args()
 
     import torch
@@ -167,6 +247,8 @@ def main():
     from substrate_bn import Context
     from oracle import oracle as O
 
+    if args.workload in ("g2validate", "g2decompress", "gtpow"):
+        return codec_workload(args, local_rank)
     if args.workload != "pairing":
         return other_workload(args, local_rank)
 

@@ -98,6 +98,56 @@ typedef enum {
 } bn_fq12_op;
 int bn_fq12_op_many(bn_ctx* ctx, int op, const bn_gt* a, const bn_gt* b, size_t n, bn_gt* out);
 
+/* ---- encodings, validation, square roots, decompression, Gt::pow ----
+ * Batched forms of the reference's per-element API.  Each element gets a status
+ * (bn_elem_status) where the reference returns a Result/Option; an element that
+ * fails has an all-zero output image.  Byte records are the reference's slices:
+ * 32-byte big-endian Fq/Fr, 64-byte big-endian Fq2 (a U512 = c1 * p + c0),
+ * 33-byte compressed G1, 65-byte compressed G2, packed back to back.  The host
+ * forms copy through the context; the _dev forms take device pointers and
+ * enqueue on `stream` (NULL: the context's stream) without synchronizing. */
+typedef enum {
+    BN_ST_OK = 0,
+    BN_ST_FIELD_INVALID_SLICE_LENGTH = 1, /* FieldError::InvalidSliceLength (lib.rs:99-104) */
+    BN_ST_FIELD_INVALID_U512 = 2,         /* FieldError::InvalidU512Encoding */
+    BN_ST_FIELD_NOT_MEMBER = 3,           /* FieldError::NotMember */
+    BN_ST_CURVE_INVALID_ENCODING = 4,     /* CurveError::InvalidEncoding (lib.rs:106-112) */
+    BN_ST_CURVE_NOT_MEMBER = 5,           /* CurveError::NotMember */
+    BN_ST_GROUP_NOT_ON_CURVE = 6,         /* groups::Error::NotOnCurve (mod.rs:89-92) */
+    BN_ST_GROUP_NOT_IN_SUBGROUP = 7       /* groups::Error::NotInSubgroup */
+} bn_elem_status;
+
+/* Fq::from_slice (lib.rs:154-159): NotMember unless the value is below p */
+int bn_fq_from_slice_many(bn_ctx* ctx, const uint8_t* be32, size_t n, bn_fq* out, uint8_t* status);
+/* Fq::to_big_endian (lib.rs:160-170): the canonical integer */
+int bn_fq_to_big_endian_many(bn_ctx* ctx, const bn_fq* a, size_t n, uint8_t* be32);
+/* Fq2::from_slice (lib.rs:260-267): c0 = v mod p, c1 = v div p; NotMember when v >= p^2 */
+int bn_fq2_from_slice_many(bn_ctx* ctx, const uint8_t* be64, size_t n, bn_fq2* out, uint8_t* status);
+/* Fr::from_slice (lib.rs:45-49): new_mul_factor, reduces any 256-bit value mod r */
+int bn_fr_from_slice_many(bn_ctx* ctx, const uint8_t* be32, size_t n, bn_fr* out);
+/* Fr::to_big_endian (lib.rs:50-55): writes the RAW Montgomery image, as the reference does */
+int bn_fr_to_big_endian_many(bn_ctx* ctx, const bn_fr* a, size_t n, uint8_t* be32);
+/* Fq::sqrt / Fq2::sqrt (fp.rs:245-260, fq2.rs:208-224): ok[i] = 0 where the reference returns None */
+int bn_fq_sqrt_many(bn_ctx* ctx, const bn_fq* a, size_t n, bn_fq* out, uint8_t* ok);
+int bn_fq2_sqrt_many(bn_ctx* ctx, const bn_fq2* a, size_t n, bn_fq2* out, uint8_t* ok);
+/* AffineG1::new / AffineG2::new (lib.rs:413-415, 549-551; mod.rs:95-113) then into G1/G2
+ * (to_jacobian, mod.rs:220-226).  G2 includes the order check [r]P == 0. */
+int bn_g1_affine_new_many(bn_ctx* ctx, const bn_fq* x, const bn_fq* y, size_t n, bn_g1* out, uint8_t* status);
+int bn_g2_affine_new_many(bn_ctx* ctx, const bn_fq2* x, const bn_fq2* y, size_t n, bn_g2* out, uint8_t* status);
+int bn_g2_affine_new_many_dev(bn_ctx* ctx, const bn_fq2* d_x, const bn_fq2* d_y, size_t n, bn_g2* d_out,
+                              uint8_t* d_status, void* stream);
+/* G1::from_compressed (lib.rs:359-375, 33-byte records) and G2::from_compressed
+ * (lib.rs:506-526, 65-byte records, includes the G2 order check) */
+int bn_g1_from_compressed_many(bn_ctx* ctx, const uint8_t* b33, size_t n, bn_g1* out, uint8_t* status);
+int bn_g2_from_compressed_many(bn_ctx* ctx, const uint8_t* b65, size_t n, bn_g2* out, uint8_t* status);
+int bn_g1_from_compressed_many_dev(bn_ctx* ctx, const uint8_t* d_b33, size_t n, bn_g1* d_out, uint8_t* d_status,
+                                   void* stream);
+int bn_g2_from_compressed_many_dev(bn_ctx* ctx, const uint8_t* d_b65, size_t n, bn_g2* d_out, uint8_t* d_status,
+                                   void* stream);
+/* out[i] = Gt::pow(a[i], k[i]) (lib.rs:592-594; generic Fq12 pow, fields/mod.rs:35-46) */
+int bn_gt_pow_many(bn_ctx* ctx, const bn_gt* a, const bn_fr* k, size_t n, bn_gt* out);
+int bn_gt_pow_many_dev(bn_ctx* ctx, const bn_gt* d_a, const bn_fr* d_k, size_t n, bn_gt* d_out, void* stream);
+
 /* ---- measurement ---- */
 /* enable HIP-event timing of each kernel phase of bn_pairing_many_dev (events are
  * recorded on the launch stream between the kernels) */

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <array>
+#include <initializer_list>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -289,6 +290,49 @@ static int host_mul(bn_ctx* c, const P* p, const bn_fr* k, size_t n, P* out, K k
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return BN_OK;
 }
+
+// ---------------------------------------------------------------- staged per-element calls
+// Host-buffer form of a one-lane-per-element kernel: chunks of kChunk elements
+// are copied in, `launch(dev, m, stream)` runs, outputs are copied back.  Each
+// buffer is described by its per-element byte size.
+struct HostIn { const void* p; size_t elem; };
+struct HostOut { void* p; size_t elem; };
+template <class Launch>
+static int staged(bn_ctx* c, size_t n, std::initializer_list<HostIn> ins, std::initializer_list<HostOut> outs,
+                  Launch&& launch) {
+    if (n == 0) return BN_OK;
+    for (const auto& b : ins)
+        if (!b.p) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    for (const auto& b : outs)
+        if (!b.p) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        size_t bytes = 0;
+        for (const auto& b : ins) bytes += (b.elem * m + 255) & ~(size_t)255;
+        for (const auto& b : outs) bytes += (b.elem * m + 255) & ~(size_t)255;
+        RET_IF(stage(c, bytes));
+        std::vector<void*> dev;
+        uint8_t* at = (uint8_t*)c->stage;
+        for (const auto& b : ins) {
+            HIPCHK(c, hipMemcpyAsync(at, (const uint8_t*)b.p + off * b.elem, m * b.elem, hipMemcpyHostToDevice, c->stream));
+            dev.push_back(at);
+            at += (b.elem * m + 255) & ~(size_t)255;
+        }
+        for (const auto& b : outs) {
+            dev.push_back(at);
+            at += (b.elem * m + 255) & ~(size_t)255;
+        }
+        RET_IF(launch(dev.data(), m, c->stream));
+        HIPCHK(c, hipGetLastError());
+        size_t k = ins.size();
+        for (const auto& b : outs) {
+            HIPCHK(c, hipMemcpyAsync((uint8_t*)b.p + off * b.elem, dev[k++], m * b.elem, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return BN_OK;
+}
+#define KL(kernel, ...) kernel<<<grid_for(m), kBlock, 0, s>>>(__VA_ARGS__)
 
 extern "C" {
 
@@ -634,6 +678,135 @@ int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n,
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     return BN_OK;
+}
+
+// ---------------------------------------------------------------- encodings / validation
+int bn_fq_from_slice_many(bn_ctx* c, const uint8_t* be32, size_t n, bn_fq* out, uint8_t* st) {
+    CTX_GUARD(c);
+    return staged(c, n, {{be32, 32}}, {{out, sizeof(bn_fq)}, {st, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_fq_from_slice, (const uint8_t*)d[0], m, (bn_fq*)d[1], (uint8_t*)d[2]);
+        return BN_OK;
+    });
+}
+int bn_fq_to_big_endian_many(bn_ctx* c, const bn_fq* a, size_t n, uint8_t* be32) {
+    CTX_GUARD(c);
+    return staged(c, n, {{a, sizeof(bn_fq)}}, {{be32, 32}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_fq_to_be, (const bn_fq*)d[0], m, (uint8_t*)d[1]);
+        return BN_OK;
+    });
+}
+int bn_fq2_from_slice_many(bn_ctx* c, const uint8_t* be64, size_t n, bn_fq2* out, uint8_t* st) {
+    CTX_GUARD(c);
+    return staged(c, n, {{be64, 64}}, {{out, sizeof(bn_fq2)}, {st, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_fq2_from_slice, (const uint8_t*)d[0], m, (bn_fq2*)d[1], (uint8_t*)d[2]);
+        return BN_OK;
+    });
+}
+int bn_fr_from_slice_many(bn_ctx* c, const uint8_t* be32, size_t n, bn_fr* out) {
+    CTX_GUARD(c);
+    return staged(c, n, {{be32, 32}}, {{out, sizeof(bn_fr)}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_fr_from_slice, (const uint8_t*)d[0], m, (bn_fr*)d[1]);
+        return BN_OK;
+    });
+}
+int bn_fr_to_big_endian_many(bn_ctx* c, const bn_fr* a, size_t n, uint8_t* be32) {
+    CTX_GUARD(c);
+    return staged(c, n, {{a, sizeof(bn_fr)}}, {{be32, 32}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_fr_to_be, (const bn_fr*)d[0], m, (uint8_t*)d[1]);
+        return BN_OK;
+    });
+}
+int bn_fq_sqrt_many(bn_ctx* c, const bn_fq* a, size_t n, bn_fq* out, uint8_t* ok) {
+    CTX_GUARD(c);
+    return staged(c, n, {{a, sizeof(bn_fq)}}, {{out, sizeof(bn_fq)}, {ok, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_fq_sqrt, (const bn_fq*)d[0], m, (bn_fq*)d[1], (uint8_t*)d[2]);
+        return BN_OK;
+    });
+}
+int bn_fq2_sqrt_many(bn_ctx* c, const bn_fq2* a, size_t n, bn_fq2* out, uint8_t* ok) {
+    CTX_GUARD(c);
+    return staged(c, n, {{a, sizeof(bn_fq2)}}, {{out, sizeof(bn_fq2)}, {ok, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_fq2_sqrt, (const bn_fq2*)d[0], m, (bn_fq2*)d[1], (uint8_t*)d[2]);
+        return BN_OK;
+    });
+}
+int bn_g1_affine_new_many(bn_ctx* c, const bn_fq* x, const bn_fq* y, size_t n, bn_g1* out, uint8_t* st) {
+    CTX_GUARD(c);
+    return staged(c, n, {{x, sizeof(bn_fq)}, {y, sizeof(bn_fq)}}, {{out, sizeof(bn_g1)}, {st, 1}},
+                  [&](void** d, size_t m, hipStream_t s) -> int {
+                      KL(k_g1_affine_new, (const bn_fq*)d[0], (const bn_fq*)d[1], m, (bn_g1*)d[2], (uint8_t*)d[3]);
+                      return BN_OK;
+                  });
+}
+int bn_g2_affine_new_many(bn_ctx* c, const bn_fq2* x, const bn_fq2* y, size_t n, bn_g2* out, uint8_t* st) {
+    CTX_GUARD(c);
+    return staged(c, n, {{x, sizeof(bn_fq2)}, {y, sizeof(bn_fq2)}}, {{out, sizeof(bn_g2)}, {st, 1}},
+                  [&](void** d, size_t m, hipStream_t s) -> int {
+                      KL(k_g2_affine_new, (const bn_fq2*)d[0], (const bn_fq2*)d[1], m, (bn_g2*)d[2], (uint8_t*)d[3]);
+                      return BN_OK;
+                  });
+}
+int bn_g2_affine_new_many_dev(bn_ctx* c, const bn_fq2* d_x, const bn_fq2* d_y, size_t n, bn_g2* d_out, uint8_t* d_st,
+                              void* stream) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!d_x || !d_y || !d_out || !d_st) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    k_g2_affine_new<<<grid_for(n), kBlock, 0, pick(c, stream)>>>(d_x, d_y, n, d_out, d_st);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+int bn_g1_from_compressed_many(bn_ctx* c, const uint8_t* b33, size_t n, bn_g1* out, uint8_t* st) {
+    CTX_GUARD(c);
+    return staged(c, n, {{b33, 33}}, {{out, sizeof(bn_g1)}, {st, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_g1_from_compressed, (const uint8_t*)d[0], m, (bn_g1*)d[1], (uint8_t*)d[2]);
+        return BN_OK;
+    });
+}
+int bn_g2_from_compressed_many(bn_ctx* c, const uint8_t* b65, size_t n, bn_g2* out, uint8_t* st) {
+    CTX_GUARD(c);
+    return staged(c, n, {{b65, 65}}, {{out, sizeof(bn_g2)}, {st, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
+        KL(k_g2_from_compressed, (const uint8_t*)d[0], m, (bn_g2*)d[1], (uint8_t*)d[2]);
+        return BN_OK;
+    });
+}
+int bn_g1_from_compressed_many_dev(bn_ctx* c, const uint8_t* d_b, size_t n, bn_g1* d_out, uint8_t* d_st, void* stream) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!d_b || !d_out || !d_st) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    k_g1_from_compressed<<<grid_for(n), kBlock, 0, pick(c, stream)>>>(d_b, n, d_out, d_st);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+int bn_g2_from_compressed_many_dev(bn_ctx* c, const uint8_t* d_b, size_t n, bn_g2* d_out, uint8_t* d_st, void* stream) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!d_b || !d_out || !d_st) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    k_g2_from_compressed<<<grid_for(n), kBlock, 0, pick(c, stream)>>>(d_b, n, d_out, d_st);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+// Gt::pow: the per-lane window table lives in the context's Fq12 slots (16 of kFeSlots)
+int bn_gt_pow_many_dev(bn_ctx* c, const bn_gt* d_a, const bn_fr* d_k, size_t n, bn_gt* d_out, void* stream) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!d_a || !d_k || !d_out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    RET_IF(reserve(c, n < kChunk ? n : kChunk));
+    hipStream_t s = pick(c, stream);
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        KL(k_gt_pow, d_a + off, d_k + off, m, d_out + off, c->slots);
+        HIPCHK(c, hipGetLastError());
+    }
+    return BN_OK;
+}
+int bn_gt_pow_many(bn_ctx* c, const bn_gt* a, const bn_fr* k, size_t n, bn_gt* out) {
+    CTX_GUARD(c);
+    return staged(c, n, {{a, sizeof(bn_gt)}, {k, sizeof(bn_fr)}}, {{out, sizeof(bn_gt)}},
+                  [&](void** d, size_t m, hipStream_t s) -> int {
+                      RET_IF(reserve(c, m));
+                      KL(k_gt_pow, (const bn_gt*)d[0], (const bn_fr*)d[1], m, (bn_gt*)d[2], c->slots);
+                      return BN_OK;
+                  });
 }
 
 }  // extern "C"

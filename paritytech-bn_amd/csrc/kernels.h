@@ -86,16 +86,17 @@ __device__ __forceinline__ auto fq6_mul_g(const Fq6<A>& a, G&& g) {
     }
 }
 
-// a * b (fq12.rs:319-327 Karatsuba) with b read per Fq2 from `yl`, the calling
-// lane's lane-strided copy of an Fq12 in LDS (word w at yl[w * kBlock]);
-// conj_b multiplies by conj(b) instead (fq12.rs:126-128).
-__device__ __forceinline__ Fq12<kF> mul12_lds(const Fq12<kF>& a, const uint32_t* yl, bool conj_b) {
+// a * b (fq12.rs:319-327 Karatsuba) with b read per Fq2 from `y`, the calling
+// lane's strided copy of an Fq12 (word w at y[w * stride]: an LDS image with
+// stride kBlock, or a lane-strided HBM slot with stride n); conj_b multiplies
+// by conj(b) instead (fq12.rs:126-128).  b is never held in registers whole.
+__device__ __forceinline__ Fq12<kF> mul12_strided(const Fq12<kF>& a, const uint32_t* y, size_t stride, bool conj_b) {
     auto ld = [&](int j) {  // Fq2 coordinate j of b (0..2: b.c0, 3..5: b.c1)
         Fq2<kF> r;
 #pragma unroll
         for (int l = 0; l < 9; ++l) {
-            r.c0.v[l] = yl[((2 * j) * 9 + l) * kBlock];
-            r.c1.v[l] = yl[((2 * j + 1) * 9 + l) * kBlock];
+            r.c0.v[l] = y[((2 * j) * 9 + l) * stride];
+            r.c1.v[l] = y[((2 * j + 1) * 9 + l) * stride];
         }
         return r;
     };
@@ -111,6 +112,9 @@ __device__ __forceinline__ Fq12<kF> mul12_lds(const Fq12<kF>& a, const uint32_t*
     const auto bb = fq6_fold(fq6_mul_g(a.c1, g1));
     const auto t = fq6_mul_g(s, gs);
     return narrow12<kF>(mk12(fq6_add(fq6_mul_by_nonresidue(bb), aa), fq6_sub(fq6_sub(t, aa), bb)));
+}
+__device__ __forceinline__ Fq12<kF> mul12_lds(const Fq12<kF>& a, const uint32_t* yl, bool conj_b) {
+    return mul12_strided(a, yl, kBlock, conj_b);
 }
 
 // Asynchronous copy of a lane-strided Fq12 (108 words, stride n) from global
@@ -262,5 +266,19 @@ __global__ void __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g,
 __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict__ f, size_t n, size_t stride, bn_gt* __restrict__ g);
 __global__ void __launch_bounds__(kBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g1* __restrict__ out);
 __global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g2* __restrict__ out);
+__global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, const bn_fr* __restrict__ k, size_t n,
+                                                   bn_gt* __restrict__ out, uint32_t* __restrict__ ws);
+// kernels_codec.hip (codec.h): encodings, square roots, validation, decompression
+__global__ void __launch_bounds__(kBlock) k_fq_from_slice(const uint8_t* __restrict__ be, size_t n, bn_fq* __restrict__ out, uint8_t* __restrict__ st);
+__global__ void __launch_bounds__(kBlock) k_fq_to_be(const bn_fq* __restrict__ a, size_t n, uint8_t* __restrict__ be);
+__global__ void __launch_bounds__(kBlock) k_fq2_from_slice(const uint8_t* __restrict__ be, size_t n, bn_fq2* __restrict__ out, uint8_t* __restrict__ st);
+__global__ void __launch_bounds__(kBlock) k_fr_from_slice(const uint8_t* __restrict__ be, size_t n, bn_fr* __restrict__ out);
+__global__ void __launch_bounds__(kBlock) k_fr_to_be(const bn_fr* __restrict__ a, size_t n, uint8_t* __restrict__ be);
+__global__ void __launch_bounds__(kBlock) k_fq_sqrt(const bn_fq* __restrict__ a, size_t n, bn_fq* __restrict__ out, uint8_t* __restrict__ ok);
+__global__ void __launch_bounds__(kBlock) k_fq2_sqrt(const bn_fq2* __restrict__ a, size_t n, bn_fq2* __restrict__ out, uint8_t* __restrict__ ok);
+__global__ void __launch_bounds__(kBlock) k_g1_affine_new(const bn_fq* __restrict__ x, const bn_fq* __restrict__ y, size_t n, bn_g1* __restrict__ out, uint8_t* __restrict__ st);
+__global__ void __launch_bounds__(kBlock) k_g2_affine_new(const bn_fq2* __restrict__ x, const bn_fq2* __restrict__ y, size_t n, bn_g2* __restrict__ out, uint8_t* __restrict__ st);
+__global__ void __launch_bounds__(kBlock) k_g1_from_compressed(const uint8_t* __restrict__ b, size_t n, bn_g1* __restrict__ out, uint8_t* __restrict__ st);
+__global__ void __launch_bounds__(kBlock) k_g2_from_compressed(const uint8_t* __restrict__ b, size_t n, bn_g2* __restrict__ out, uint8_t* __restrict__ st);
 
 }  // namespace bn

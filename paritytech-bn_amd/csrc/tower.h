@@ -57,7 +57,10 @@ BN_INLINE auto fq2_dbl(const Fq2<B>& a) { return fq2_add(a, a); }
 template <int B>
 BN_INLINE Fq2<2> fq2_fold(const Fq2<B>& a) { return {fq_fold(a.c0), fq_fold(a.c1)}; }
 template <int B>
-BN_INLINE bool fq2_is_zero(const Fq2<B>& a) { return fq_is_zero(a.c0) & fq_is_zero(a.c1); }
+BN_INLINE bool fq2_is_zero(const Fq2<B>& a) {
+    const bool z0 = fq_is_zero(a.c0), z1 = fq_is_zero(a.c1);
+    return z0 && z1;
+}
 // x unchanged when its bound is <= L, else folded to 2 (decided at compile time)
 template <int L, int B>
 BN_INLINE auto pre(const Fq<B>& a) {
@@ -68,7 +71,10 @@ BN_INLINE auto pre(const Fq2<B>& a) {
     if constexpr (kv(B) <= L) return a; else return fq2_fold(a);
 }
 template <int A, int B>
-BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) { return fq_eq(a.c0, b.c0) & fq_eq(a.c1, b.c1); }
+BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) {
+    const bool e0 = fq_eq(a.c0, b.c0), e1 = fq_eq(a.c1, b.c1);
+    return e0 && e1;
+}
 
 template <int B>
 BN_INLINE Fq2<kv(B)> fq2_norm(const Fq2<B>& a) { return {fq_norm(a.c0), fq_norm(a.c1)}; }

@@ -10,6 +10,15 @@ Same names and argument meaning as the Rust crate for the batched hot path:
     G1 * Fr, G2 * Fr                                   lib.rs:425-431, 575-581
     Gt * Gt                                            lib.rs:603-609
 
+and the wire formats and validation around it:
+
+    Fq.from_slice / to_big_endian / sqrt               lib.rs:154-183
+    Fq2.from_slice / sqrt                              lib.rs:238-267
+    Fr.from_slice / to_big_endian                      lib.rs:45-55
+    AffineG1.new, AffineG2.new (curve + order check)   lib.rs:413-415, 549-551
+    G1.from_compressed, G2.from_compressed             lib.rs:359-375, 506-526
+    Gt.pow(Fr)                                         lib.rs:592-594
+
 plus the batched forms the reference lacks (pairing_many, g1_mul_many) that
 the engine exists for.  Values keep the reference's memory images (canonical
 Montgomery, little-endian u64 limbs), so a Gt compares equal exactly when the
@@ -28,8 +37,25 @@ R_ORDER = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
 _RM = 1 << 256
 
 
+class FieldError(Exception):
+    """lib.rs:99-104: InvalidSliceLength, InvalidU512Encoding, NotMember (args[0])."""
+
+
 class CurveError(Exception):
-    """lib.rs:110-116 -- ToAffineConversion is the only variant the path raises."""
+    """lib.rs:106-116: InvalidEncoding, NotMember, Field(FieldError), ToAffineConversion (args[0])."""
+
+
+class GroupError(Exception):
+    """groups/mod.rs:89-92: NotOnCurve, NotInSubgroup (args[0])."""
+
+
+_FIELD = {1: "InvalidSliceLength", 2: "InvalidU512Encoding", 3: "NotMember"}
+
+
+def _curve_error(st):
+    if st in _FIELD:
+        return CurveError("Field", FieldError(_FIELD[st]))
+    return CurveError({4: "InvalidEncoding", 5: "NotMember"}[st])
 
 
 _ctx = None
@@ -80,8 +106,85 @@ class Fr:
     def __neg__(self):
         return Fr.from_int(-self.into_int())
 
+    @classmethod
+    def from_slice(cls, b):  # lib.rs:45-49: new_mul_factor reduces mod r
+        if len(b) != 32:
+            raise FieldError("InvalidSliceLength")
+        return cls(context().fr_from_slice_many(np.frombuffer(bytes(b), np.uint8))[0])
+
+    def to_big_endian(self):  # lib.rs:50-55: the raw Montgomery image
+        return bytes(context().fr_to_big_endian_many(self.img)[0])
+
     def __eq__(self, o):
         return isinstance(o, Fr) and np.array_equal(self.img, o.img)
+
+
+class Fq:
+    """Base-field element in Montgomery form (fields::Fq, fp.rs:195-222)."""
+    __slots__ = ("img",)
+
+    def __init__(self, img):
+        self.img = np.ascontiguousarray(img, dtype=np.uint64).reshape(4)
+
+    @classmethod
+    def from_int(cls, v):
+        return cls(_limbs((v % P) * _RM % P))
+
+    @classmethod
+    def from_slice(cls, b):  # lib.rs:154-159
+        if len(b) != 32:
+            raise FieldError("InvalidSliceLength")
+        out, st = context().fq_from_slice_many(np.frombuffer(bytes(b), np.uint8))
+        if st[0]:
+            raise FieldError(_FIELD[int(st[0])])
+        return cls(out[0])
+
+    def to_big_endian(self):  # lib.rs:160-170
+        return bytes(context().fq_to_big_endian_many(self.img)[0])
+
+    def sqrt(self):  # fp.rs:245-260
+        out, ok = context().fq_sqrt_many(self.img)
+        return Fq(out[0]) if ok[0] else None
+
+    def into_int(self):
+        return _int(self.img) * pow(_RM, -1, P) % P
+
+    def __eq__(self, o):
+        return isinstance(o, Fq) and np.array_equal(self.img, o.img)
+
+
+class Fq2:
+    """c0 + c1 u (fields::Fq2, fq2.rs); img = c0 limbs then c1 limbs."""
+    __slots__ = ("img",)
+
+    def __init__(self, img):
+        self.img = np.ascontiguousarray(img, dtype=np.uint64).reshape(8)
+
+    @classmethod
+    def new(cls, a, b):  # lib.rs:238-240
+        return cls(np.concatenate([a.img, b.img]))
+
+    @classmethod
+    def from_slice(cls, b):  # lib.rs:260-267
+        if len(b) != 64:
+            raise FieldError("InvalidU512Encoding")
+        out, st = context().fq2_from_slice_many(np.frombuffer(bytes(b), np.uint8))
+        if st[0]:
+            raise FieldError(_FIELD[int(st[0])])
+        return cls(out[0])
+
+    def real(self):
+        return Fq(self.img[:4])
+
+    def imaginary(self):
+        return Fq(self.img[4:])
+
+    def sqrt(self):  # fq2.rs:208-224
+        out, ok = context().fq2_sqrt_many(self.img)
+        return Fq2(out[0]) if ok[0] else None
+
+    def __eq__(self, o):
+        return isinstance(o, Fq2) and np.array_equal(self.img, o.img)
 
 
 class _Point:
@@ -117,6 +220,24 @@ class G1(_Point):
     def __mul__(self, k):
         return G1(context().g1_mul_many(self.img, k.img)[0])
 
+    @classmethod
+    def from_compressed(cls, b):  # lib.rs:359-375
+        if len(b) != 33:
+            raise CurveError("InvalidEncoding")
+        out, st = context().g1_from_compressed_many(np.frombuffer(bytes(b), np.uint8))
+        if st[0]:
+            raise _curve_error(int(st[0]))
+        return cls(out[0])
+
+    def x(self):
+        return Fq(self.img[0:4])
+
+    def y(self):
+        return Fq(self.img[4:8])
+
+    def z(self):
+        return Fq(self.img[8:12])
+
 
 class G2(_Point):
     """Jacobian G2 point over Fq2 (groups::G2, mod.rs:408-472)."""
@@ -139,6 +260,46 @@ class G2(_Point):
     def __mul__(self, k):
         return G2(context().g2_mul_many(self.img, k.img)[0])
 
+    @classmethod
+    def from_compressed(cls, b):  # lib.rs:506-526
+        if len(b) != 65:
+            raise CurveError("InvalidEncoding")
+        out, st = context().g2_from_compressed_many(np.frombuffer(bytes(b), np.uint8))
+        if st[0]:
+            raise _curve_error(int(st[0]))
+        return cls(out[0])
+
+    def x(self):
+        return Fq2(self.img[0:8])
+
+    def y(self):
+        return Fq2(self.img[8:16])
+
+    def z(self):
+        return Fq2(self.img[16:24])
+
+
+class AffineG1:
+    """lib.rs:397-433; new() validates (mod.rs:95-113, G1: curve equation only)."""
+
+    @staticmethod
+    def new(x, y):
+        out, st = context().g1_affine_new_many(x.img, y.img)
+        if st[0]:
+            raise GroupError({6: "NotOnCurve", 7: "NotInSubgroup"}[int(st[0])])
+        return G1(out[0])  # From<AffineG1> for G1 (to_jacobian)
+
+
+class AffineG2:
+    """lib.rs:533-571; new() validates the curve equation and the order (mod.rs:95-113)."""
+
+    @staticmethod
+    def new(x, y):
+        out, st = context().g2_affine_new_many(x.img, y.img)
+        if st[0]:
+            raise GroupError({6: "NotOnCurve", 7: "NotInSubgroup"}[int(st[0])])
+        return G2(out[0])
+
 
 class Gt:
     """Target group element (Gt(Fq12), lib.rs:584-609)."""
@@ -155,6 +316,9 @@ class Gt:
 
     def __mul__(self, o):
         return Gt(context().fq12_op_many("mul", self.img, o.img)[0])
+
+    def pow(self, k):  # lib.rs:592-594
+        return Gt(context().gt_pow_many(self.img, k.img)[0])
 
     def final_exponentiation(self):
         out, ok = context().final_exponentiation_many(self.img)
@@ -204,3 +368,20 @@ def g1_mul_many(p, k):
 
 def g2_mul_many(p, k):
     return context().g2_mul_many(p, k)
+
+
+def g2_affine_new_many(x, y):
+    """(G2 images, bn_elem_status) for arrays of affine (x, y): AffineG2::new batched."""
+    return context().g2_affine_new_many(x, y)
+
+
+def g1_from_compressed_many(b33):
+    return context().g1_from_compressed_many(b33)
+
+
+def g2_from_compressed_many(b65):
+    return context().g2_from_compressed_many(b65)
+
+
+def gt_pow_many(a, k):
+    return context().gt_pow_many(a, k)

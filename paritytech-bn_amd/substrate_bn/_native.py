@@ -29,7 +29,15 @@ EXPORTS = [
     "bn_final_exponentiation_many", "bn_miller_loop_many",
     "bn_g1_mul_many", "bn_g1_mul_many_dev", "bn_g2_mul_many", "bn_g2_mul_many_dev",
     "bn_fq12_op_many", "bn_workspace_bytes", "bn_reserve", "bn_set_phase_timing", "bn_get_phase_times",
+    "bn_fq_from_slice_many", "bn_fq_to_big_endian_many", "bn_fq2_from_slice_many", "bn_fr_from_slice_many",
+    "bn_fr_to_big_endian_many", "bn_fq_sqrt_many", "bn_fq2_sqrt_many", "bn_g1_affine_new_many",
+    "bn_g2_affine_new_many", "bn_g2_affine_new_many_dev", "bn_g1_from_compressed_many", "bn_g2_from_compressed_many",
+    "bn_g1_from_compressed_many_dev", "bn_g2_from_compressed_many_dev", "bn_gt_pow_many", "bn_gt_pow_many_dev",
 ]
+
+# per-element status (bn_elem_status)
+ST_OK, ST_FIELD_INVALID_SLICE_LENGTH, ST_FIELD_INVALID_U512, ST_FIELD_NOT_MEMBER = 0, 1, 2, 3
+ST_CURVE_INVALID_ENCODING, ST_CURVE_NOT_MEMBER, ST_GROUP_NOT_ON_CURVE, ST_GROUP_NOT_IN_SUBGROUP = 4, 5, 6, 7
 
 
 class BnError(RuntimeError):
@@ -71,6 +79,22 @@ def load():
         "bn_reserve": ([vp, sz], i),
         "bn_set_phase_timing": ([vp, i], i),
         "bn_get_phase_times": ([vp, vp, vp], i),
+        "bn_fq_from_slice_many": ([vp, vp, sz, vp, vp], i),
+        "bn_fq_to_big_endian_many": ([vp, vp, sz, vp], i),
+        "bn_fq2_from_slice_many": ([vp, vp, sz, vp, vp], i),
+        "bn_fr_from_slice_many": ([vp, vp, sz, vp], i),
+        "bn_fr_to_big_endian_many": ([vp, vp, sz, vp], i),
+        "bn_fq_sqrt_many": ([vp, vp, sz, vp, vp], i),
+        "bn_fq2_sqrt_many": ([vp, vp, sz, vp, vp], i),
+        "bn_g1_affine_new_many": ([vp, vp, vp, sz, vp, vp], i),
+        "bn_g2_affine_new_many": ([vp, vp, vp, sz, vp, vp], i),
+        "bn_g2_affine_new_many_dev": ([vp, vp, vp, sz, vp, vp, vp], i),
+        "bn_g1_from_compressed_many": ([vp, vp, sz, vp, vp], i),
+        "bn_g2_from_compressed_many": ([vp, vp, sz, vp, vp], i),
+        "bn_g1_from_compressed_many_dev": ([vp, vp, sz, vp, vp, vp], i),
+        "bn_g2_from_compressed_many_dev": ([vp, vp, sz, vp, vp, vp], i),
+        "bn_gt_pow_many": ([vp, vp, vp, sz, vp], i),
+        "bn_gt_pow_many_dev": ([vp, vp, vp, sz, vp, vp], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -200,6 +224,105 @@ class Context:
         cnt = np.zeros(1, np.int32)
         self._check(self._L.bn_get_phase_times(self._h, _ptr(ms), _ptr(cnt)))
         return ms.astype(float), int(cnt[0])
+
+    # ---- encodings / validation / square roots / decompression / Gt::pow
+    def _bytes_in(self, b, width):
+        b = np.ascontiguousarray(b, dtype=np.uint8)
+        if b.size % width:
+            raise ValueError("byte buffer of %d is not a multiple of %d" % (b.size, width))
+        return b.reshape(-1, width)
+
+    def fq_from_slice_many(self, be32):
+        b = self._bytes_in(be32, 32)
+        out = np.zeros((b.shape[0], 4), np.uint64)
+        st = np.zeros(b.shape[0], np.uint8)
+        self._check(self._L.bn_fq_from_slice_many(self._h, _ptr(b), b.shape[0], _ptr(out), _ptr(st)))
+        return out, st
+
+    def fq_to_big_endian_many(self, a):
+        a = _arr(a, 4)
+        out = np.zeros((a.shape[0], 32), np.uint8)
+        self._check(self._L.bn_fq_to_big_endian_many(self._h, _ptr(a), a.shape[0], _ptr(out)))
+        return out
+
+    def fq2_from_slice_many(self, be64):
+        b = self._bytes_in(be64, 64)
+        out = np.zeros((b.shape[0], 8), np.uint64)
+        st = np.zeros(b.shape[0], np.uint8)
+        self._check(self._L.bn_fq2_from_slice_many(self._h, _ptr(b), b.shape[0], _ptr(out), _ptr(st)))
+        return out, st
+
+    def fr_from_slice_many(self, be32):
+        b = self._bytes_in(be32, 32)
+        out = np.zeros((b.shape[0], 4), np.uint64)
+        self._check(self._L.bn_fr_from_slice_many(self._h, _ptr(b), b.shape[0], _ptr(out)))
+        return out
+
+    def fr_to_big_endian_many(self, a):
+        a = _arr(a, 4)
+        out = np.zeros((a.shape[0], 32), np.uint8)
+        self._check(self._L.bn_fr_to_big_endian_many(self._h, _ptr(a), a.shape[0], _ptr(out)))
+        return out
+
+    def fq_sqrt_many(self, a):
+        a = _arr(a, 4)
+        out = np.zeros_like(a)
+        ok = np.zeros(a.shape[0], np.uint8)
+        self._check(self._L.bn_fq_sqrt_many(self._h, _ptr(a), a.shape[0], _ptr(out), _ptr(ok)))
+        return out, ok
+
+    def fq2_sqrt_many(self, a):
+        a = _arr(a, 8)
+        out = np.zeros_like(a)
+        ok = np.zeros(a.shape[0], np.uint8)
+        self._check(self._L.bn_fq2_sqrt_many(self._h, _ptr(a), a.shape[0], _ptr(out), _ptr(ok)))
+        return out, ok
+
+    def g1_affine_new_many(self, x, y):
+        x, y = _arr(x, 4), _arr(y, 4)
+        out = np.zeros((x.shape[0], 12), np.uint64)
+        st = np.zeros(x.shape[0], np.uint8)
+        self._check(self._L.bn_g1_affine_new_many(self._h, _ptr(x), _ptr(y), x.shape[0], _ptr(out), _ptr(st)))
+        return out, st
+
+    def g2_affine_new_many(self, x, y):
+        x, y = _arr(x, 8), _arr(y, 8)
+        out = np.zeros((x.shape[0], 24), np.uint64)
+        st = np.zeros(x.shape[0], np.uint8)
+        self._check(self._L.bn_g2_affine_new_many(self._h, _ptr(x), _ptr(y), x.shape[0], _ptr(out), _ptr(st)))
+        return out, st
+
+    def g1_from_compressed_many(self, b33):
+        b = self._bytes_in(b33, 33)
+        out = np.zeros((b.shape[0], 12), np.uint64)
+        st = np.zeros(b.shape[0], np.uint8)
+        self._check(self._L.bn_g1_from_compressed_many(self._h, _ptr(b), b.shape[0], _ptr(out), _ptr(st)))
+        return out, st
+
+    def g2_from_compressed_many(self, b65):
+        b = self._bytes_in(b65, 65)
+        out = np.zeros((b.shape[0], 24), np.uint64)
+        st = np.zeros(b.shape[0], np.uint8)
+        self._check(self._L.bn_g2_from_compressed_many(self._h, _ptr(b), b.shape[0], _ptr(out), _ptr(st)))
+        return out, st
+
+    def gt_pow_many(self, a, k):
+        a, k = _arr(a, 48), _arr(k, 4)
+        out = np.zeros_like(a)
+        self._check(self._L.bn_gt_pow_many(self._h, _ptr(a), _ptr(k), a.shape[0], _ptr(out)))
+        return out
+
+    def g2_affine_new_many_dev(self, d_x, d_y, n, d_out, d_st, stream=None):
+        self._check(self._L.bn_g2_affine_new_many_dev(self._h, d_x, d_y, n, d_out, d_st, stream))
+
+    def g1_from_compressed_many_dev(self, d_b, n, d_out, d_st, stream=None):
+        self._check(self._L.bn_g1_from_compressed_many_dev(self._h, d_b, n, d_out, d_st, stream))
+
+    def g2_from_compressed_many_dev(self, d_b, n, d_out, d_st, stream=None):
+        self._check(self._L.bn_g2_from_compressed_many_dev(self._h, d_b, n, d_out, d_st, stream))
+
+    def gt_pow_many_dev(self, d_a, d_k, n, d_out, stream=None):
+        self._check(self._L.bn_gt_pow_many_dev(self._h, d_a, d_k, n, d_out, stream))
 
     def reserve(self, n):
         self._check(self._L.bn_reserve(self._h, n))

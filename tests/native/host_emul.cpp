@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include "../../paritytech-bn_amd/csrc/codec.h"
 #include "../../paritytech-bn_amd/csrc/pairing.h"
 
 using namespace bn;
@@ -82,5 +83,63 @@ void he_g2_mul(const uint32_t* p, const uint32_t* k_canonical, uint32_t* o) {
     G2J a = {widen<kPt>(ld2(p)), widen<kPt>(ld2(p + 16)), widen<kPt>(ld2(p + 32))};
     G2J r = jac_mul(a, k_canonical);
     st2(r.x, o); st2(r.y, o + 16); st2(r.z, o + 32);
+}
+// ---- codec.h (encodings, sqrt, validation, decompression)
+int he_fq_from_slice(const uint8_t* be, uint32_t* o) {
+    uint32_t w[8];
+    words_from_be<8>(be, w);
+    Fq<2> x;
+    bool ok = fq_new_plain(w, x);
+    st(x, o);
+    return ok ? ST_OK : ST_FIELD_NOT_MEMBER;
+}
+void he_fq_to_be(const uint32_t* a, uint8_t* be) {
+    uint32_t w[8];
+    fq_plain_words(ld(a), w);
+    be_from_words<8>(w, be);
+}
+int he_fq2_from_slice(const uint8_t* be, uint32_t* o) {
+    uint32_t v[16];
+    words_from_be<16>(be, v);
+    Fq2<2> x;
+    bool ok = fq2_from_u512(v, x);
+    st2(x, o);
+    return ok ? ST_OK : ST_FIELD_NOT_MEMBER;
+}
+void he_fr_from_slice(const uint8_t* be, uint32_t* o) {
+    uint32_t w[8];
+    words_from_be<8>(be, w);
+    fr_from_plain_words(w, o);
+}
+int he_fq_sqrt(const uint32_t* a, uint32_t* o) {
+    Fq<2> r;
+    bool some = fq_sqrt(ld(a), r);
+    st(r, o);
+    return some;
+}
+int he_fq2_sqrt(const uint32_t* a, uint32_t* o) {
+    Fq2<kPt> r;
+    bool some = fq2_sqrt(ld2(a), r);
+    st2(r, o);
+    return some;
+}
+int he_g2_affine_new(const uint32_t* xy, uint32_t* o) {
+    Fq2<kPt> x = widen<kPt>(ld2(xy)), y = widen<kPt>(ld2(xy + 16));
+    if (!g2_on_curve(x, y)) return ST_GROUP_NOT_ON_CURVE;
+    if (!g2_in_subgroup(x, y)) return ST_GROUP_NOT_IN_SUBGROUP;
+    st2(x, o); st2(y, o + 16); st2(fq2_one(), o + 32);
+    return ST_OK;
+}
+int he_g1_from_compressed(const uint8_t* b, uint32_t* o) {
+    Fq<2> x, y;
+    uint8_t s = g1_decompress(b, x, y);
+    if (s == ST_OK) { st(x, o); st(y, o + 8); st(fq_one(), o + 16); }
+    return s;
+}
+int he_g2_from_compressed(const uint8_t* b, uint32_t* o) {
+    Fq2<kPt> x, y;
+    uint8_t s = g2_decompress(b, x, y);
+    if (s == ST_OK) { st2(x, o); st2(y, o + 16); st2(fq2_one(), o + 32); }
+    return s;
 }
 }
