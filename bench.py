@@ -147,7 +147,7 @@ def codec_workload(args, local_rank):
 
     dev = torch.device("cuda", local_rank)
     ctx = Context(local_rank)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # a real stream: handle 0 would mean the context's own stream
     sh = stream.cuda_stream
     n = args.pairs
     threads = min(16, os.cpu_count() or 1)
@@ -255,7 +255,11 @@ def main():
     n = args.pairs
     ctx = Context(local_rank)
     ctx.reserve(n)
-    stream = torch.cuda.current_stream(dev)
+    # One real (non-default) stream for the engine's kernels, torch's copies and the
+    # RCCL all-gather, so the collective is ordered after the pairings it gathers
+    # (handle 0 would send the kernels to the context's own non-blocking stream).
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
 
     # ---- synthetic inputs in HBM (engine kernels; Jacobian images)
