@@ -15,6 +15,12 @@
 #pragma once
 #include "fq.h"
 
+// Fq2 product form used by fq2_mul: 1 = schoolbook with lazy reduction
+// (fq2_mul_sb), 0 = Karatsuba with lazy reduction (fq2_mul_lazy)
+#ifndef BN_FQ2_SB
+#define BN_FQ2_SB 1
+#endif
+
 namespace bn {
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
@@ -158,6 +164,69 @@ BN_INLINE auto fq2_mul_lazy(const Fq2<A>& a, const Fq2<B>& b) {
     }
 }
 
+// Fq2 product by schoolbook with one Montgomery reduction per output
+// coordinate and no subtraction: c0 = a0*b0 - a1*b1 is accumulated as
+// a0*b0 + a1*(K*p - b1), where K*p - b1 (kp_spread, K = B + 1) has non-negative
+// digits below (Lb+2)*2^29, so both coordinates are plain unsigned column sums
+// of 2 x 81 products plus their 81-product reduction: 486 multiply-adds and no
+// 64-bit adds or subtracts (on gfx950 a carry op costs as much as a
+// multiply-add).  Column sums: c0 < 9*(La*Lb + La*(Lb+2) + 1)*2^58 + 2^35 and
+// c1 < 9*(2*La*Lb + 1)*2^58 + 2^35, both below 2^64 when La*(2*Lb+2) <= 6;
+// the operands are swapped (the product commutes) or normalized otherwise.
+template <int A, int B>
+BN_INLINE auto fq2_mul_sb(const Fq2<A>& a, const Fq2<B>& b) {
+    if constexpr (kl(A) * (2 * kl(B) + 2) > 6) {
+        if constexpr (kl(B) * (2 * kl(A) + 2) <= 6) return fq2_mul_sb(b, a);
+        else if constexpr (kl(A) >= kl(B)) return fq2_mul_sb(fq2_norm(a), b);
+        else return fq2_mul_sb(a, fq2_norm(b));
+    } else {
+    static_assert(kv(A) <= 40 && kv(B) <= 40, "fq2_mul_sb bound");
+    constexpr Limbs9 NQ = kp_spread(kv(B) + 1, kl(B));
+    constexpr int B0 = 1 + (int)(((long long)kv(A) * (2 * kv(B) + 1) * 5908 + 999999) / 1000000);
+    constexpr int B1 = 1 + (int)(((long long)2 * kv(A) * kv(B) * 5908 + 999999) / 1000000);
+    uint32_t nb[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nb[i] = NQ.v[i] - b.c1.v[i];
+    uint32_t m0[9], m1[9];
+    Fq<B0> c0;
+    Fq<B1> c1;
+    uint64_t acc0 = 0, acc1 = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        const int lo = k < 9 ? 0 : k - 8;
+        const int hi = k < 9 ? k : 8;
+#pragma unroll
+        for (int i = lo; i <= hi; ++i) {
+            acc0 += (uint64_t)a.c0.v[i] * b.c0.v[k - i];
+            acc1 += (uint64_t)a.c0.v[i] * b.c1.v[k - i];
+            acc0 += (uint64_t)a.c1.v[i] * nb[k - i];
+            acc1 += (uint64_t)a.c1.v[i] * b.c0.v[k - i];
+        }
+#pragma unroll
+        for (int i = lo; i <= hi; ++i) {
+            if (i < k) {
+                acc0 += (uint64_t)m0[i] * kP29.v[k - i];
+                acc1 += (uint64_t)m1[i] * kP29.v[k - i];
+            }
+        }
+        if (k < 9) {
+            m0[k] = ((uint32_t)acc0 * BN_PINV29) & M29;
+            m1[k] = ((uint32_t)acc1 * BN_PINV29) & M29;
+            acc0 += (uint64_t)m0[k] * kP29.v[0];
+            acc1 += (uint64_t)m1[k] * kP29.v[0];
+        } else {
+            c0.v[k - 9] = (uint32_t)acc0 & M29;
+            c1.v[k - 9] = (uint32_t)acc1 & M29;
+        }
+        acc0 >>= 29;
+        acc1 >>= 29;
+    }
+    c0.v[8] = (uint32_t)acc0;
+    c1.v[8] = (uint32_t)acc1;
+    return mk2(c0, c1);
+    }
+}
+
 // fq2.rs:136-148: the same product (Karatsuba, bb * (p-1) + aa == aa - bb)
 template <int A, int B>
 BN_INLINE auto fq2_mul(const Fq2<A>& a_in, const Fq2<B>& b_in) {
@@ -166,7 +235,11 @@ BN_INLINE auto fq2_mul(const Fq2<A>& a_in, const Fq2<B>& b_in) {
     Fq2<B> b = b_in;
     fq2_fence(a);
     fq2_fence(b);
+#if BN_FQ2_SB
+    auto r = fq2_mul_sb(a, b);
+#else
     auto r = fq2_mul_lazy(a, b);
+#endif
     fq2_fence(r);
     return r;
     }
