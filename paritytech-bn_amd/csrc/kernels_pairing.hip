@@ -25,14 +25,22 @@ __global__ void __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p,
     if ((p_zero || q_zero) && mode == 1) atomicOr(err, 1 << BN_ERR_TO_AFFINE);
     flags[i] = (p_zero || q_zero) ? 1 : 0;
 
-    auto pzinv = fq_inv(pz);
+    // One inversion for both points (Montgomery's trick): t = (pz * N(qz))^-1 with
+    // N(qz) = qz.c0^2 + qz.c1^2 (the norm fq2.rs:119-130 inverts), so pz^-1 = t * N(qz)
+    // and qz^-1 = conj(qz) * (t * pz).  Inverses are unique: these are the values the
+    // reference's two inversions give.  A zero z makes t = 0; that pair is skipped
+    // (flags) or rejected (mode 1) and its values are never used.
+    const auto nq = fq_add(fq_sqr(qz.c0), fq_sqr(qz.c1));
+    const Fq<2> t = fq_inv_w(fq_mul(pz, nq));
+    const auto pzinv = fq_mul(t, nq);
+    const auto ninv = fq_mul(t, pz);
     auto pzinv2 = fq_sqr(pzinv);
     auto px = fq_mul(ld_ref(p[i].x), pzinv2);
     auto py = fq_mul(ld_ref(p[i].y), fq_mul(pzinv2, pzinv));
     st_fq(paff, n, i, 0, px);
     st_fq(paff, n, i, 1, py);
 
-    auto qzinv = fq2_inv(qz);
+    const auto qzinv = mk2(fq_mul(qz.c0, ninv), fq_neg(fq_mul(qz.c1, ninv)));
     auto qzinv2 = fq2_sqr(qzinv);
     G2Aff<kPt> qa = {narrow<kPt>(fq2_mul(ld_ref2(q[i].x), qzinv2)),
                      narrow<kPt>(fq2_mul(ld_ref2(q[i].y), fq2_mul(qzinv2, qzinv)))};

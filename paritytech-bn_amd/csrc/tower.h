@@ -276,25 +276,100 @@ BN_INLINE auto fq2_conj(const Fq2<B>& a) { return mk2(a.c0, fq_neg(a.c1)); }
 // ---------------------------------------------------------------- inversion
 // Fermat: a^(p-2).  Inverses are unique, so this equals the reference's binary
 // extended Euclid (arith.rs:324-370 + fp.rs:108-117) bit for bit, without its
-// data-dependent control flow.  The exponent bit is uniform across the wave.
-BN_INLINE bool pm2_bit(int bit) {  // bits of p - 2
-    const uint64_t w = bit >= 192 ? 0x30644e72e131a029ull
-                     : bit >= 128 ? 0xb85045b68181585dull
-                     : bit >= 64  ? 0x97816a916871ca8dull
-                                  : 0x3c208c16d87cfd45ull;
-    return (w >> (bit & 63)) & 1u;
+// data-dependent control flow.  The chain is the windowed plan below (fq_inv_w).
+// ---------------------------------------------------------------- fixed-exponent windowed powers
+// Left-to-right sliding window of width 4 for a constant exponent, planned at
+// compile time as (squarings, odd digit) steps.  The exponent is the same in
+// every lane, so the digit dispatch is a scalar branch.  x^e is unique, so any
+// chain gives the reference's value (fields/mod.rs:35-46 square-and-multiply).
+struct PowPlan {
+    int first = 0, n = 0;
+    uint8_t sq[96] = {};
+    uint8_t dig[96] = {};
+};
+constexpr bool pbit(const uint64_t (&e)[4], int i) { return (e[i >> 6] >> (i & 63)) & 1u; }
+constexpr PowPlan pow_plan(const uint64_t (&e)[4], int top) {
+    PowPlan c;
+    int i = top, pend = 0;
+    bool first = true;
+    while (i >= 0) {
+        if (!pbit(e, i)) {
+            ++pend;
+            --i;
+            continue;
+        }
+        int j = i - 3 < 0 ? 0 : i - 3;
+        while (!pbit(e, j)) ++j;
+        int v = 0;
+        for (int k = i; k >= j; --k) v = 2 * v + (pbit(e, k) ? 1 : 0);
+        if (first) {
+            c.first = v;
+            first = false;
+        } else {
+            c.sq[c.n] = (uint8_t)(pend + i - j + 1);
+            c.dig[c.n] = (uint8_t)v;
+            ++c.n;
+        }
+        pend = 0;
+        i = j - 1;
+    }
+    if (pend) {
+        c.sq[c.n] = (uint8_t)pend;
+        c.dig[c.n] = 0;
+        ++c.n;
+    }
+    return c;
 }
+constexpr uint64_t kPm2[4] = {0x3c208c16d87cfd45ull, 0x97816a916871ca8dull, 0xb85045b68181585dull,
+                              0x30644e72e131a029ull};  // p - 2
+constexpr PowPlan kInvPlan = pow_plan(kPm2, 253);
+
 template <int B>
-BN_INLINE Fq<2> fq_inv(const Fq<B>& a) {
-    const Fq<2> x = widen<2>(fq_reduce(a));
-    Fq<2> r = x;  // bit 253 (top bit of p-2) is set
+BN_INLINE Fq<2> fq_pow_plan(const Fq<B>& a, const PowPlan& c) {
+    const Fq<2> x1 = widen<2>(fq_reduce(a));
+    const Fq<2> x2 = fq_sqr(x1);
+    const Fq<2> x3 = fq_mul(x1, x2), x5 = fq_mul(x3, x2), x7 = fq_mul(x5, x2), x9 = fq_mul(x7, x2);
+    const Fq<2> x11 = fq_mul(x9, x2), x13 = fq_mul(x11, x2), x15 = fq_mul(x13, x2);
+    auto times = [&](const Fq<2>& r, int d) -> Fq<2> {
+        switch (d) {
+            case 1: return fq_mul(r, x1);
+            case 3: return fq_mul(r, x3);
+            case 5: return fq_mul(r, x5);
+            case 7: return fq_mul(r, x7);
+            case 9: return fq_mul(r, x9);
+            case 11: return fq_mul(r, x11);
+            case 13: return fq_mul(r, x13);
+            case 15: return fq_mul(r, x15);
+            default: return r;
+        }
+    };
+    Fq<2> r;
+    switch (c.first) {
+        case 1: r = x1; break;
+        case 3: r = x3; break;
+        case 5: r = x5; break;
+        case 7: r = x7; break;
+        case 9: r = x9; break;
+        case 11: r = x11; break;
+        case 13: r = x13; break;
+        default: r = x15; break;
+    }
 #pragma unroll 1
-    for (int bit = 252; bit >= 0; --bit) {
-        r = fq_sqr(r);
-        if (pm2_bit(bit)) r = fq_mul(r, x);
+    for (int s = 0; s < c.n; ++s) {
+        const int q = c.sq[s];
+#pragma unroll 1
+        for (int k = 0; k < q; ++k) r = fq_sqr(r);
+        r = times(r, c.dig[s]);
     }
     return r;
 }
+// Fermat inversion a^(p-2) by the windowed plan (253 squarings, ~55 products
+// instead of the binary chain's ~126): the same unique inverse
+template <int B>
+BN_INLINE Fq<2> fq_inv_w(const Fq<B>& a) { return fq_pow_plan(a, kInvPlan); }
+template <int B>
+BN_INLINE Fq<2> fq_inv(const Fq<B>& a) { return fq_inv_w(a); }
+
 // fq2.rs:119-130
 template <int B>
 BN_INLINE auto fq2_inv(const Fq2<B>& a_in) {
