@@ -53,6 +53,44 @@ __device__ __forceinline__ Fq12<B> ld_fq12(const uint32_t* base, size_t n, size_
             {ld_fq2<B>(base, n, i, 6), ld_fq2<B>(base, n, i, 8), ld_fq2<B>(base, n, i, 10)}};
 }
 
+// In the step machine, Fq12 slots go through a buffer descriptor (the *_buf forms):
+// one 32-bit VGPR offset (the lane) serves all 108 words, and the word offset
+// w * n * 4 is the uniform scalar soffset.  Plain global loads of a
+// lane-strided element need a 64-bit VGPR address per word.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slot_rsrc(const uint32_t* base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+}
+template <int B>
+__device__ __forceinline__ Fq<B> ld_fq_buf(__amdgpu_buffer_rsrc_t rs, int vo, size_t n, int j) {
+    Fq<B> x;
+#pragma unroll
+    for (int l = 0; l < 9; ++l) x.v[l] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, (int)(((size_t)j * 9 + l) * n * 4), 0);
+    return x;
+}
+template <int B>
+__device__ __forceinline__ void st_fq_buf(__amdgpu_buffer_rsrc_t rs, int vo, size_t n, int j, const Fq<B>& x) {
+#pragma unroll
+    for (int l = 0; l < 9; ++l) __builtin_amdgcn_raw_buffer_store_b32(x.v[l], rs, vo, (int)(((size_t)j * 9 + l) * n * 4), 0);
+}
+template <int B>
+__device__ __forceinline__ void st_fq12_buf(uint32_t* base, size_t n, size_t i, const Fq12<B>& f) {
+    const auto rs = slot_rsrc(base);
+    const int vo = (int)(i * 4);
+    const Fq2<B>* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        st_fq_buf(rs, vo, n, 2 * k, c[k]->c0);
+        st_fq_buf(rs, vo, n, 2 * k + 1, c[k]->c1);
+    }
+}
+template <int B>
+__device__ __forceinline__ Fq12<B> ld_fq12_buf(const uint32_t* base, size_t n, size_t i) {
+    const auto rs = slot_rsrc(base);
+    const int vo = (int)(i * 4);
+    auto q = [&](int k) { return Fq2<B>{ld_fq_buf<B>(rs, vo, n, 2 * k), ld_fq_buf<B>(rs, vo, n, 2 * k + 1)}; };
+    return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
+}
+
 template <int B>
 __device__ __forceinline__ Fq6<B> ld_fq6(const uint32_t* base, size_t n, size_t i, int h) {
     return {ld_fq2<B>(base, n, i, 6 * h), ld_fq2<B>(base, n, i, 6 * h + 2), ld_fq2<B>(base, n, i, 6 * h + 4)};

@@ -18,18 +18,24 @@ __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__
         const uint32_t ins = prog[2 * pc];  // uniform: scalar loads
         const uint32_t aux = prog[2 * pc + 1];
         const uint32_t op = ins & 0xff, k = aux & 0xff, flags = aux >> 8;
-        uint32_t* d = slot_ptr(slots, n, (ins >> 8) & 0xff);
-        const uint32_t* a = slot_ptr(slots, n, (ins >> 16) & 0xff);
-        const uint32_t* b = slot_ptr(slots, n, ins >> 24);
+        // The slot stride passes through an empty asm once per step, so the 108
+        // word offsets of a lane-strided Fq12 (w * n, uniform) are rebuilt where
+        // they are used instead of being hoisted out of the step loop, where they
+        // would occupy ~216 SGPRs and spill through VGPR lanes.
+        size_t nn = n;
+        asm volatile("" : "+s"(nn));
+        uint32_t* d = slot_ptr(slots, nn, (ins >> 8) & 0xff);
+        const uint32_t* a = slot_ptr(slots, nn, (ins >> 16) & 0xff);
+        const uint32_t* b = slot_ptr(slots, nn, ins >> 24);
         Fq12<kF> x;
-        if (flags & kFlagAccA) x = acc; else x = ld_fq12<kF>(a, n, i);
+        if (flags & kFlagAccA) x = acc; else x = ld_fq12_buf<kF>(a, nn, i);
         Fq12<kF> r;
         switch (op) {
             case OP_MOV: r = x; break;
             case OP_MUL: {
 #pragma unroll 1
                 for (uint32_t j = 0; j < k; ++j) x = cyc_sqr(x);
-                Fq12<kF> y = ld_fq12<kF>(b, n, i);
+                Fq12<kF> y = ld_fq12_buf<kF>(b, nn, i);
                 if (flags & kFlagConjB) y = fq12_conj(y);
                 r = mul12(x, y);
                 if (flags & kFlagConjOut) r = fq12_conj(r);
@@ -49,7 +55,7 @@ __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__
             default: r = narrow12<kF>(fq12_inv(x)); break;  // OP_INV
         }
         acc = r;
-        if (!(flags & kFlagNoStore)) st_fq12(d, n, i, r);
+        if (!(flags & kFlagNoStore)) st_fq12_buf(d, nn, i, r);
     }
 }
 

@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libbn254mi.so")
+LIB_PATH = os.environ.get("BN254MI_LIB") or os.path.join(PKG_DIR, "libbn254mi.so")  # override: A/B builds
 
 BN_OK = 0
 BN_ERR_INVALID_ARGUMENT = 1
