@@ -207,18 +207,24 @@ __device__ __forceinline__ void st_ref2(bn_fq2& a, const Fq2<B>& x) {
 }
 template <int B>
 __device__ __forceinline__ void st_gt(bn_gt& g, const Fq12<B>& f) {
-    const Fq2<B>* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        st_ref(g.c[2 * k], c[k]->c0);
-        st_ref(g.c[2 * k + 1], c[k]->c1);
-    }
+    // coefficient order c0.c0.c0, c0.c0.c1, c0.c1.c0, ... (fq12.rs:52-55); no array
+    // of pointers (a private array would live in scratch)
+    st_ref(g.c[0], f.c0.c0.c0);
+    st_ref(g.c[1], f.c0.c0.c1);
+    st_ref(g.c[2], f.c0.c1.c0);
+    st_ref(g.c[3], f.c0.c1.c1);
+    st_ref(g.c[4], f.c0.c2.c0);
+    st_ref(g.c[5], f.c0.c2.c1);
+    st_ref(g.c[6], f.c1.c0.c0);
+    st_ref(g.c[7], f.c1.c0.c1);
+    st_ref(g.c[8], f.c1.c1.c0);
+    st_ref(g.c[9], f.c1.c1.c1);
+    st_ref(g.c[10], f.c1.c2.c0);
+    st_ref(g.c[11], f.c1.c2.c1);
 }
 __device__ __forceinline__ Fq12<2> ld_gt(const bn_gt& g) {
-    Fq2<2> c[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) c[k] = {ld_ref(g.c[2 * k]), ld_ref(g.c[2 * k + 1])};
-    return {{c[0], c[1], c[2]}, {c[3], c[4], c[5]}};
+    auto q = [&](int k) { return Fq2<2>{ld_ref(g.c[2 * k]), ld_ref(g.c[2 * k + 1])}; };
+    return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
 }
 __device__ __forceinline__ void st_gt_zero(bn_gt& g) {
     uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};

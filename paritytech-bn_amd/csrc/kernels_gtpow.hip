@@ -15,21 +15,34 @@ __global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, 
                                                    bn_gt* __restrict__ out, uint32_t* __restrict__ ws) {
     const size_t i = lane_id();
     if (i >= n) return;
-    auto slot = [&](uint32_t t) { return ws + (size_t)t * kSlotWords * n; };
+    // slot access through a buffer descriptor with the stride laundered per use
+    // (kernels.h, as in the step machine): no hoisted per-word offsets
+    auto slot = [&](uint32_t t, size_t nn) { return ws + (size_t)t * kSlotWords * nn; };
+    auto stride = [&]() {
+        size_t nn = n;
+        asm volatile("" : "+s"(nn));
+        return nn;
+    };
     const Fq12<kF> x = widen<kF>(ld_gt(a[i]));
-    st_fq12(slot(0), n, i, widen<kF>(fq12_one()));
-    st_fq12(slot(1), n, i, x);
+    {
+        const size_t nn = stride();
+        st_fq12_buf(slot(0, nn), nn, i, widen<kF>(fq12_one()));
+        st_fq12_buf(slot(1, nn), nn, i, x);
+    }
     Fq12<kF> t = x;
 #pragma unroll 1
     for (uint32_t j = 2; j < 16; ++j) {
-        mem_fence();
-        t = mul12(t, ld_fq12<kF>(slot(1), n, i));
-        st_fq12(slot(j), n, i, t);
+        const size_t nn = stride();
+        t = mul12(t, ld_fq12_buf<kF>(slot(1, nn), nn, i));
+        st_fq12_buf(slot(j, nn), nn, i, t);
     }
     uint32_t e[8];
     fr_to_canonical(k[i], e);  // U256::from(Fr), fp.rs:13-20
-    mem_fence();
-    Fq12<kF> acc = ld_fq12<kF>(slot(e[7] >> 28), n, i);
+    Fq12<kF> acc;
+    {
+        const size_t nn = stride();
+        acc = ld_fq12_buf<kF>(slot(e[7] >> 28, nn), nn, i);
+    }
 #pragma unroll 1
     for (int w = 62; w >= 0; --w) {
 #pragma unroll
@@ -37,8 +50,8 @@ __global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, 
         e[0] <<= 4;
 #pragma unroll 1
         for (int s = 0; s < 4; ++s) acc = narrow12<kF>(fq12_sqr(acc));
-        mem_fence();
-        acc = mul12(acc, ld_fq12<kF>(slot(e[7] >> 28), n, i));
+        const size_t nn = stride();
+        acc = mul12(acc, ld_fq12_buf<kF>(slot(e[7] >> 28, nn), nn, i));
     }
     st_gt(out[i], acc);
 }

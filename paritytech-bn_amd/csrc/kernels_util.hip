@@ -7,9 +7,9 @@ namespace bn {
 __global__ void __launch_bounds__(kBlock) k_fq12_product(uint32_t* __restrict__ f, size_t stride, size_t m, size_t half) {
     const size_t i = lane_id();
     if (i >= half || i + half >= m) return;
-    Fq12<kF> a = ld_fq12<kF>(f, stride, i);
-    Fq12<kF> b = ld_fq12<kF>(f, stride, i + half);
-    st_fq12(f, stride, i, mul12(a, b));
+    Fq12<kF> a = ld_fq12_buf<kF>(f, stride, i);
+    Fq12<kF> b = ld_fq12_buf<kF>(f, stride, i + half);
+    st_fq12_buf(f, stride, i, mul12(a, b));
 }
 
 // Gt images <-> lane-strided internal Fq12

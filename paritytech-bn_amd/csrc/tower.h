@@ -20,6 +20,10 @@
 #ifndef BN_FQ2_SB
 #define BN_FQ2_SB 1
 #endif
+// 1: the Fq6 product issues its six Fq2 products as three fenced pairs
+#ifndef BN_FQ6_PAIRS
+#define BN_FQ6_PAIRS 1
+#endif
 
 namespace bn {
 
@@ -84,10 +88,19 @@ BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) {
 
 template <int B>
 BN_INLINE Fq2<kv(B)> fq2_norm(const Fq2<B>& a) { return {fq_norm(a.c0), fq_norm(a.c1)}; }
+// BN_FQ2_FENCE = 0 lets the compiler interleave independent Fq2 products
+// (more ILP, more live registers); 1 serializes them in program order.
+#ifndef BN_FQ2_FENCE
+#define BN_FQ2_FENCE 1
+#endif
 template <int B>
 BN_INLINE void fq2_fence(Fq2<B>& a) {
+#if BN_FQ2_FENCE
     fq_fence(a.c0);
     fq_fence(a.c1);
+#else
+    (void)a;
+#endif
 }
 
 // fq2.rs:48-53
@@ -244,6 +257,35 @@ BN_INLINE auto fq2_mul(const Fq2<A>& a_in, const Fq2<B>& b_in) {
     return r;
     }
 }
+// Two independent Fq2 products computed together: the fences bracket the
+// pair, so the two column sums interleave (twice the independent multiply-add
+// chains for one wave) while no more than two products are in flight.
+template <class R, class S>
+struct Fq2Pair {
+    R a;
+    S b;
+};
+template <int A, int B, int C, int D>
+BN_INLINE auto fq2_mul2(const Fq2<A>& a_in, const Fq2<B>& b_in, const Fq2<C>& c_in, const Fq2<D>& d_in) {
+    if constexpr (kv(A) > 40 || kv(B) > 40 || kv(C) > 40 || kv(D) > 40) {
+        return fq2_mul2(pre<40>(a_in), pre<40>(b_in), pre<40>(c_in), pre<40>(d_in));
+    } else {
+        Fq2<A> a = a_in;
+        Fq2<B> b = b_in;
+        Fq2<C> c = c_in;
+        Fq2<D> d = d_in;
+        fq2_fence(a);
+        fq2_fence(b);
+        fq2_fence(c);
+        fq2_fence(d);
+        auto r = fq2_mul_sb(a, b);
+        auto q = fq2_mul_sb(c, d);
+        fq2_fence(r);
+        fq2_fence(q);
+        return Fq2Pair<decltype(r), decltype(q)>{r, q};
+    }
+}
+
 // fq2.rs:105-117: (c1*(p-1) + c0)(c0 + c1) - ab - ab*(p-1) == (c0 - c1)(c0 + c1); c1 = 2ab
 template <int A>
 BN_INLINE auto fq2_sqr(const Fq2<A>& a_in) {
@@ -416,12 +458,25 @@ BN_INLINE auto fq6_mul_by_nonresidue(const Fq6<B>& a) { return mk6(fq2_mul_xi(a.
 template <int A, int B>
 BN_INLINE auto fq6_mul(const Fq6<A>& a, const Fq6<B>& b) {
     if constexpr (kv(A) > 20 || kv(B) > 20) return fq6_mul(pre<20>(a), pre<20>(b)); else {
+#if BN_FQ6_PAIRS
+    // the six Fq2 products in three independent pairs
+    const auto p1 = fq2_mul2(a.c0, b.c0, a.c1, b.c1);
+    const auto& a_a = p1.a;
+    const auto& b_b = p1.b;
+    const auto p2 = fq2_mul2(a.c2, b.c2, fq2_add(a.c1, a.c2), fq2_add(b.c1, b.c2));
+    const auto& c_c = p2.a;
+    auto t0 = fq2_sub(fq2_sub(p2.b, b_b), c_c);
+    const auto p3 = fq2_mul2(fq2_add(a.c0, a.c1), fq2_add(b.c0, b.c1), fq2_add(a.c0, a.c2), fq2_add(b.c0, b.c2));
+    auto t1 = fq2_sub(fq2_sub(p3.a, a_a), b_b);
+    auto t2 = fq2_sub(p3.b, a_a);
+#else
     auto a_a = fq2_mul(a.c0, b.c0);
     auto b_b = fq2_mul(a.c1, b.c1);
     auto c_c = fq2_mul(a.c2, b.c2);
     auto t0 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c1, a.c2), fq2_add(b.c1, b.c2)), b_b), c_c);
     auto t1 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c0, a.c1), fq2_add(b.c0, b.c1)), a_a), b_b);
     auto t2 = fq2_sub(fq2_mul(fq2_add(a.c0, a.c2), fq2_add(b.c0, b.c2)), a_a);
+#endif
     return mk6(fq2_add(fq2_mul_xi(t0), a_a), fq2_add(t1, fq2_mul_xi(c_c)), fq2_sub(fq2_add(t2, b_b), c_c));
     }
 }
