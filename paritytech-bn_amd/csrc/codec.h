@@ -231,25 +231,46 @@ BN_INLINE bool g2_on_curve(const Fq2<X>& x, const Fq2<Y>& y) {
     return fq2_eq(fq2_sqr(y), fq2_add(fq2_mul(fq2_sqr(x), x), g2_coeff_b()));
 }
 
-// NAF of r (constants.inc): [r]P by 254 doublings and 73 additions of +-P
-constexpr uint64_t kRNafNz[4] = BN_RNAF_NZ;
-constexpr uint64_t kRNafNeg[4] = BN_RNAF_NEG;
+// Projective equality with the reference's zero handling (mod.rs:169-195)
+template <template <int> class F>
+BN_INLINE bool jac_eq(const Jac<F>& a, const Jac<F>& b) {
+    const bool az = jac_is_zero(a), bz = jac_is_zero(b);
+    const auto z1s = F_sqr(a.z), z2s = F_sqr(b.z);
+    const bool ex = F_is_zero(F_sub(F_mul(a.x, z2s), F_mul(b.x, z1s)));
+    const bool ey = F_is_zero(F_sub(F_mul(a.y, F_mul(b.z, z2s)), F_mul(b.y, F_mul(a.z, z1s))));
+    return az ? bz : (!bz && ex && ey);
+}
+
+// NAF of the trace t = 6u^2 + 1 (constants.inc)
+constexpr uint64_t kTNafNz[4] = BN_TNAF_NZ;
+constexpr uint64_t kTNafNeg[4] = BN_TNAF_NEG;
 
 // The order check of AffineG<G2Params>::new (mod.rs:99-108): the reference
-// tests p * (-1) + p == 0, i.e. [r]P == 0; evaluated here by the NAF of r with
-// the reference's own complete Jacobian law (mod.rs:250-334: zero inputs,
-// doubling and P + (-P) are all handled), so the boolean is the same.
+// tests p * (-1) + p == 0, i.e. [r]P == 0.  On the twist the Frobenius map
+// psi (the reference's mul_by_q, mod.rs:694-699) satisfies psi^2 - t psi + p = 0
+// on every point, and r = p + 1 - t, so
+//     [r]P = [t](psi(P) - P) - (psi^2(P) - P)
+// exactly, and [r]P == 0 <=> [t](psi(P) - P) == psi^2(P) - P: the same boolean
+// from a 127-bit chain instead of a 254-bit one.  (tools/psi_check.py checks
+// the identity and both outcomes with plain integers.)  The group law is the
+// reference's complete Jacobian one (mod.rs:250-334).
 template <int B>
 BN_INLINE bool g2_in_subgroup(const Fq2<B>& x, const Fq2<B>& y) {
-    const G2J p = {narrow<kPt>(x), narrow<kPt>(y), widen<kPt>(fq2_one())};
-    const G2J pn = {p.x, narrow<kPt>(fq2_neg(p.y)), p.z};
-    G2J acc = p;  // top digit (+1)
+    const G2Aff<kPt> p0 = {narrow<kPt>(x), narrow<kPt>(y)};
+    const G2Aff<kPt> p1 = mul_by_q(p0);  // psi(P)
+    const G2Aff<kPt> p2 = mul_by_q(p1);  // psi^2(P)
+    const Fq2<kPt> one = widen<kPt>(fq2_one());
+    const G2J pn = {p0.x, narrow<kPt>(fq2_neg(p0.y)), one};
+    const G2J q = jac_add(G2J{p1.x, p1.y, one}, pn);  // psi(P) - P
+    const G2J s = jac_add(G2J{p2.x, p2.y, one}, pn);  // psi^2(P) - P
+    const G2J qn = jac_neg(q);
+    G2J acc = q;  // top digit (+1)
 #pragma unroll 1
-    for (int bit = BN_RNAF_TOP - 1; bit >= 0; --bit) {
+    for (int bit = BN_TNAF_TOP - 1; bit >= 0; --bit) {
         acc = jac_double(acc);
-        if (ebit(kRNafNz, bit)) acc = jac_add(acc, ebit(kRNafNeg, bit) ? pn : p);
+        if (ebit(kTNafNz, bit)) acc = jac_add(acc, ebit(kTNafNeg, bit) ? qn : q);
     }
-    return jac_is_zero(acc);
+    return jac_eq(acc, s);
 }
 
 // canonical y > canonical(-y) as Fq2::to_u512 values c1 * p + c0 (lib.rs:517, fq2.rs:226-231):

@@ -192,3 +192,10 @@ def test_gt_pow_matches_repeated_products():
     # g^(r-1) * g == 1 for a pairing output (order r)
     one = O.binary("orc_fq12_mul", out[1], g[1], 48, 48, 48)[0]
     assert canon(one) == [1] + [0] * 11
+
+
+def test_psi_identity_behind_the_g2_order_check():
+    """codec.h decides [r]P == 0 as [t](psi(P) - P) == psi^2(P) - P; the identity
+    (psi^2 - t psi + p = 0 on the whole twist) is checked with plain integers."""
+    import runpy
+    runpy.run_path(os.path.join(os.path.dirname(__file__), "..", "tools", "psi_check.py"), run_name="psi_check")
