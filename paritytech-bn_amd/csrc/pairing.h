@@ -8,7 +8,7 @@
 namespace bn {
 
 // storage bound of the Miller accumulator and of the final-exponentiation temporaries
-constexpr int kF = 4;
+constexpr int kF = 2;
 template <int S, int B>
 BN_INLINE Fq12<S> narrow12(const Fq12<B>& a) {
     if constexpr (kv(B) <= S) {
