@@ -219,13 +219,14 @@ struct G2Proj {
 
 // mod.rs:754-776 -- the twist() * i product is xi * i (ring identity)
 BN_INLINE Ell doubling_step(G2Proj& s) {
-    auto a = fq2_scale(fq2_mul(s.x, s.y), two_inv());
+    // x * two_inv is the halving x / 2 mod p: the same residue, no product
+    auto a = fq2_half(fq2_mul(s.x, s.y));
     auto b = fq2_sqr(s.y);
     auto c = fq2_sqr(s.z);
     auto d = fq2_add(fq2_add(c, c), c);
     auto e = fq2_mul(g2_coeff_b(), d);
     auto f = fq2_add(fq2_add(e, e), e);
-    auto g = fq2_scale(fq2_add(b, f), two_inv());
+    auto g = fq2_half(fq2_add(b, f));
     auto h = fq2_sub(fq2_sqr(fq2_add(s.y, s.z)), fq2_add(b, c));
     auto i = fq2_sub(e, b);
     auto j = fq2_sqr(s.x);

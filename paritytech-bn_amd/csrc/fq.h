@@ -273,6 +273,31 @@ BN_INLINE auto fq_mul_small(const Fq<B>& a) {
     }
 }
 
+// x / 2 mod p, the residue of x * two_inv (groups/mod.rs:521-528) without a
+// product: add p when x is odd (after normalizing), carry, then shift every
+// digit right by one bit, taking the low bit of the next digit.  A value
+// <= B*p becomes <= (B+1)/2 * p.
+template <int K>
+BN_INLINE auto fq_half(const Fq<K>& a_in) {
+    constexpr int B = kv(K);
+    static_assert(B + 1 <= 161, "fq_half: x + p must stay below 2^261");
+    const Fq<B> a = fq_norm(a_in);
+    const uint32_t mask = 0u - (a.v[0] & 1u);
+    uint32_t t[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t[i] = a.v[i] + (kP29.v[i] & mask);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        t[i + 1] += t[i] >> 29;
+        t[i] &= M29;
+    }
+    Fq<(B + 2) / 2> r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.v[i] = (t[i] >> 1) | ((t[i + 1] & 1u) << 28);
+    r.v[8] = t[8] >> 1;
+    return r;
+}
+
 // Partial reduction to bound 2 without a multiplication: estimate
 // q <= floor(x/p) from the top digit (x8 * 2^232 / p, computed in f32 with a
 // constant rounded 2^-18 low so the estimate never overshoots), then x - q*p.

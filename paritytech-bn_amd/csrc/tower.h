@@ -103,6 +103,8 @@ BN_INLINE void fq2_fence(Fq2<B>& a) {
 #endif
 }
 
+template <int B>
+BN_INLINE auto fq2_half(const Fq2<B>& a) { return mk2(fq_half(a.c0), fq_half(a.c1)); }
 // fq2.rs:48-53
 template <int A, int B>
 BN_INLINE auto fq2_scale(const Fq2<A>& a, const Fq<B>& s) { return mk2(fq_mul(a.c0, s), fq_mul(a.c1, s)); }
