@@ -10,10 +10,14 @@ Writes profiles/TAG_kernel_stats.csv              (per-kernel launches, average 
        profiles/pmc_summary.json                  (bench.py reads roofline.traffic from it)
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  Per MI355X_MICROARCH.md §HBM,
-FETCH_SIZE counts half the bytes of 16-B/lane streaming reads; this engine's
-workspace accesses are 4-B/lane coalesced dwords (256 B per wave instruction),
-an access width the guide lists as uncalibrated, so the raw value x 1024 is
-reported and the caveat recorded with it.
+FETCH_SIZE counts half the bytes of 16-B/lane streaming reads and must be
+doubled; WRITE_SIZE is exact.  This engine's workspace accesses are 4-B/lane
+coalesced dwords, which the guide leaves uncalibrated, so they are calibrated
+here on k_fe_out, whose bytes are known exactly: per pairing it reads two
+lane-strided Fq12 slots (2 x 432 B) plus one flag byte and writes one 384 B Gt
+image.  The measured FETCH_SIZE / expected read bytes gives the read factor
+(0.51 on gfx950, i.e. the same one-half), WRITE_SIZE / expected write bytes
+checks the writes (1.00).  hbm_bytes_per_launch = FETCH / factor + WRITE.
 """
 import collections
 import csv
@@ -63,6 +67,15 @@ for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
     # counters_collection holds one row per (dispatch, counter), already summed over instances
     for kname, cname, val in db.execute("select kernel_name, counter_name, value from counters_collection"):
         agg[short(kname)][cname].append(float(val))
+# read calibration on k_fe_out (n pairings: 2 * 432 + 1 bytes read, 384 written)
+cal = agg.get("k_fe_out", {})
+read_factor, write_factor = None, None
+if cal.get("FETCH_SIZE") and cal.get("WRITE_SIZE"):
+    n_cal = 65536  # bench.py's default batch (pairs per GPU)
+    read_factor = (sum(cal["FETCH_SIZE"]) / len(cal["FETCH_SIZE"]) * 1024) / (n_cal * (2 * 432 + 1))
+    write_factor = (sum(cal["WRITE_SIZE"]) / len(cal["WRITE_SIZE"]) * 1024) / (n_cal * 384)
+    print("calibration on k_fe_out: FETCH_SIZE/expected reads = %.3f, WRITE_SIZE/expected writes = %.3f"
+          % (read_factor, write_factor))
 summary = {}
 lines = ["%-16s %14s %14s %14s %12s %10s" % ("kernel", "FETCH_bytes", "WRITE_bytes", "VALU/wave", "WAVE_CYC/w",
                                                  "VALU/cyc")]
@@ -75,12 +88,14 @@ for k, v in sorted(agg.items()):
     waves = m.get("SQ_WAVES", 0) or 1
     valu = m.get("SQ_INSTS_VALU", 0) / waves
     cyc = m.get("SQ_WAVE_CYCLES", 0) * 4 / waves  # quad-cycles -> cycles
-    summary[k] = {"hbm_bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+    corr = (fetch / read_factor if read_factor else fetch) + write
+    summary[k] = {"hbm_bytes_per_launch": corr, "fetch_bytes_raw": fetch, "write_bytes": write,
+                  "read_factor": read_factor, "write_factor": write_factor,
                   "valu_insts_per_wave": valu, "wave_cycles": cyc,
                   "valu_per_cycle_per_wave": valu / cyc if cyc else None,
                   "grbm_gui_active": m.get("GRBM_GUI_ACTIVE"),
-                  "note": "FETCH_SIZE/WRITE_SIZE raw (KiB*1024); 4-B/lane dword accesses are uncalibrated "
-                          "(MI355X_MICROARCH §HBM); source %s" % tag}
+                  "note": "FETCH_SIZE corrected by the read factor calibrated on k_fe_out (known bytes), "
+                          "WRITE_SIZE as counted (MI355X_MICROARCH §HBM); source %s" % tag}
     lines.append("%-16s %14.3e %14.3e %14.3e %12.3e %10.3f" % (k, fetch, write, valu, cyc, valu / cyc if cyc else 0))
 if summary:
     json.dump(summary, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
