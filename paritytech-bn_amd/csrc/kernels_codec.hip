@@ -30,6 +30,7 @@ __device__ __forceinline__ void zero_fq(bn_fq& a) {
 // Fq::from_slice (lib.rs:154-159)
 __global__ void __launch_bounds__(kBlock) k_fq_from_slice(const uint8_t* __restrict__ be, size_t n, bn_fq* __restrict__ out,
                                                           uint8_t* __restrict__ st) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint32_t w[8];
@@ -41,6 +42,7 @@ __global__ void __launch_bounds__(kBlock) k_fq_from_slice(const uint8_t* __restr
 }
 // Fq::to_big_endian (lib.rs:160-170): the canonical integer
 __global__ void __launch_bounds__(kBlock) k_fq_to_be(const bn_fq* __restrict__ a, size_t n, uint8_t* __restrict__ be) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint32_t w[8];
@@ -50,6 +52,7 @@ __global__ void __launch_bounds__(kBlock) k_fq_to_be(const bn_fq* __restrict__ a
 // Fq2::from_slice (lib.rs:260-267)
 __global__ void __launch_bounds__(kBlock) k_fq2_from_slice(const uint8_t* __restrict__ be, size_t n, bn_fq2* __restrict__ out,
                                                            uint8_t* __restrict__ st) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint32_t v[16];
@@ -67,6 +70,7 @@ __global__ void __launch_bounds__(kBlock) k_fq2_from_slice(const uint8_t* __rest
 }
 // Fr::from_slice (lib.rs:45-49: new_mul_factor, reduces mod r)
 __global__ void __launch_bounds__(kBlock) k_fr_from_slice(const uint8_t* __restrict__ be, size_t n, bn_fr* __restrict__ out) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint32_t w[8], m[8];
@@ -76,6 +80,7 @@ __global__ void __launch_bounds__(kBlock) k_fr_from_slice(const uint8_t* __restr
 }
 // Fr::to_big_endian (lib.rs:50-55): the RAW Montgomery image, as the reference writes it
 __global__ void __launch_bounds__(kBlock) k_fr_to_be(const bn_fr* __restrict__ a, size_t n, uint8_t* __restrict__ be) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint32_t w[8];
@@ -86,6 +91,7 @@ __global__ void __launch_bounds__(kBlock) k_fr_to_be(const bn_fr* __restrict__ a
 // Fq::sqrt / Fq2::sqrt (fp.rs:245-260, fq2.rs:208-224); ok[i] = 0 for None
 __global__ void __launch_bounds__(kBlock) k_fq_sqrt(const bn_fq* __restrict__ a, size_t n, bn_fq* __restrict__ out,
                                                     uint8_t* __restrict__ ok) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     Fq<2> r;
@@ -95,6 +101,7 @@ __global__ void __launch_bounds__(kBlock) k_fq_sqrt(const bn_fq* __restrict__ a,
 }
 __global__ void __launch_bounds__(kBlock) k_fq2_sqrt(const bn_fq2* __restrict__ a, size_t n, bn_fq2* __restrict__ out,
                                                      uint8_t* __restrict__ ok) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     Fq2<kPt> r;
@@ -111,6 +118,7 @@ __global__ void __launch_bounds__(kBlock) k_fq2_sqrt(const bn_fq2* __restrict__ 
 // AffineG::new (mod.rs:95-113) -> to_jacobian (mod.rs:220-226)
 __global__ void __launch_bounds__(kBlock) k_g1_affine_new(const bn_fq* __restrict__ x, const bn_fq* __restrict__ y, size_t n,
                                                           bn_g1* __restrict__ out, uint8_t* __restrict__ st) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     const Fq<2> X = ld_ref(x[i]), Y = ld_ref(y[i]);
@@ -141,6 +149,7 @@ __device__ __forceinline__ void st_g2_affine(bn_g2& o, const Fq2<B>& x, const Fq
 }
 __global__ void __launch_bounds__(kBlock) k_g2_affine_new(const bn_fq2* __restrict__ x, const bn_fq2* __restrict__ y, size_t n,
                                                           bn_g2* __restrict__ out, uint8_t* __restrict__ st) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     const Fq2<kPt> X = widen<kPt>(ld_ref2(x[i])), Y = widen<kPt>(ld_ref2(y[i]));
@@ -154,6 +163,7 @@ __global__ void __launch_bounds__(kBlock) k_g2_affine_new(const bn_fq2* __restri
 // G1::from_compressed / G2::from_compressed (lib.rs:359-375, 506-526); records of 33 / 65 bytes
 __global__ void __launch_bounds__(kBlock) k_g1_from_compressed(const uint8_t* __restrict__ b, size_t n, bn_g1* __restrict__ out,
                                                                uint8_t* __restrict__ st) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint8_t rec[33];
@@ -174,6 +184,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_from_compressed(const uint8_t* __
 }
 __global__ void __launch_bounds__(kBlock) k_g2_from_compressed(const uint8_t* __restrict__ b, size_t n, bn_g2* __restrict__ out,
                                                                uint8_t* __restrict__ st) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint8_t rec[65];

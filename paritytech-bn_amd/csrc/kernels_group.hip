@@ -6,6 +6,7 @@ namespace bn {
 // ---------------------------------------------------------------- scalar multiplication
 __global__ void __launch_bounds__(kBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n,
                                                    bn_g1* __restrict__ out) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint32_t s[8];
@@ -18,6 +19,7 @@ __global__ void __launch_bounds__(kBlock) k_g1_mul(const bn_g1* __restrict__ p, 
 }
 __global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n,
                                                    bn_g2* __restrict__ out) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint32_t s[8];

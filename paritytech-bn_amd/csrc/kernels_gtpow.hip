@@ -13,6 +13,7 @@ namespace bn {
 
 __global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, const bn_fr* __restrict__ k, size_t n,
                                                    bn_gt* __restrict__ out, uint32_t* __restrict__ ws) {
+    fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
     // slot access through a buffer descriptor with the stride laundered per use

@@ -65,7 +65,15 @@ BN_INLINE auto fq2_neg(const Fq2<B>& a) { return mk2(fq_neg(a.c0), fq_neg(a.c1))
 template <int B>
 BN_INLINE auto fq2_dbl(const Fq2<B>& a) { return fq2_add(a, a); }
 template <int B>
-BN_INLINE Fq2<2> fq2_fold(const Fq2<B>& a) { return {fq_fold(a.c0), fq_fold(a.c1)}; }
+BN_INLINE Fq2<2> fq2_fold(const Fq2<B>& a) {
+#if BN_FOLD_LDS && defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (kl(B) <= 6) {
+        const FoldEnt e0 = fold_fetch(a.c0), e1 = fold_fetch(a.c1);
+        return {fold_apply(a.c0, e0), fold_apply(a.c1, e1)};
+    }
+#endif
+    return {fq_fold(a.c0), fq_fold(a.c1)};
+}
 template <int B>
 BN_INLINE bool fq2_is_zero(const Fq2<B>& a) {
     const bool z0 = fq_is_zero(a.c0), z1 = fq_is_zero(a.c1);
@@ -443,7 +451,17 @@ BN_INLINE auto fq6_sub(const Fq6<A>& a, const Fq6<B>& b) {
 template <int B>
 BN_INLINE auto fq6_neg(const Fq6<B>& a) { return mk6(fq2_neg(a.c0), fq2_neg(a.c1), fq2_neg(a.c2)); }
 template <int B>
-BN_INLINE Fq6<2> fq6_fold(const Fq6<B>& a) { return {fq2_fold(a.c0), fq2_fold(a.c1), fq2_fold(a.c2)}; }
+BN_INLINE Fq6<2> fq6_fold(const Fq6<B>& a) {
+#if BN_FOLD_LDS && defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (kl(B) <= 6) {
+        const FoldEnt e0 = fold_fetch(a.c0.c0), e1 = fold_fetch(a.c0.c1), e2 = fold_fetch(a.c1.c0),
+                      e3 = fold_fetch(a.c1.c1), e4 = fold_fetch(a.c2.c0), e5 = fold_fetch(a.c2.c1);
+        return {{fold_apply(a.c0.c0, e0), fold_apply(a.c0.c1, e1)}, {fold_apply(a.c1.c0, e2), fold_apply(a.c1.c1, e3)},
+                {fold_apply(a.c2.c0, e4), fold_apply(a.c2.c1, e5)}};
+    }
+#endif
+    return {fq2_fold(a.c0), fq2_fold(a.c1), fq2_fold(a.c2)};
+}
 template <int B>
 BN_INLINE Fq6<kv(B)> fq6_norm(const Fq6<B>& a) { return {fq2_norm(a.c0), fq2_norm(a.c1), fq2_norm(a.c2)}; }
 template <int B>

@@ -13,7 +13,7 @@ _lib = None
 
 def build():
     src = os.path.join(HERE, "host_emul.cpp")
-    subprocess.check_call(["g++", "-O0", "-std=c++17", "-fPIC", "-shared", "-o", SO, src])
+    subprocess.check_call(["g++", "-O0", "-std=c++17", "-DBN_HOST_CHECKS", "-fPIC", "-shared", "-o", SO, src])
 
 
 def lib():

@@ -63,6 +63,19 @@ def test_tower_vs_oracle(rnd):
         assert np.array_equal(H.call("he_fq2_sqr", x, out_words=16), O.unary("orc_fq2_squared", x, 8)[0][0])
 
 
+def test_gt_pow_formulas():
+    # k_gt_pow's window chain on a pairing output and a (non-cyclotomic) Miller value
+    p, q, _, _ = O.random_pairs(2, seed=61)
+    a = np.concatenate([O.pairing_many(p[:1], q[:1]), O.miller_loop_batch(q[1:2], p[1:2])[1][None]])
+    vals, k = O.random_scalars(2, 62, lo=0)
+    for scal in (vals[0], 0, 1, O.R - 1):
+        K = O.canon_to_mont_array([scal], O.FR).reshape(1, 4)
+        words = np.frombuffer(int(scal).to_bytes(32, "little"), np.uint64).copy()
+        for j in range(2):
+            got = H.call("he_gt_pow", a[j], words, out_words=96)
+            assert np.array_equal(got, O.gt_pow(a[j:j + 1], K)[0])
+
+
 def _frob(a, pw):
     out = np.zeros(48, np.uint64)
     O.lib().orc_fq12_frobenius_map(O._p(np.ascontiguousarray(a)), pw, O._p(out))
