@@ -48,10 +48,27 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def fr_images(n, seed):
-    from oracle import oracle as O  # host-side scalar sampling helpers only
-    vals, imgs = O.random_scalars(n, seed)
-    return imgs
+def fr_images(n, seed, lo=1):
+    from substrate_bn import synth  # product-side input sampling; oracle/ is only the checker
+    return synth.fr_images(n, seed, lo)
+
+
+def device_points(ctx, n, seed_g1, seed_g2, dev, sh):
+    """P_i = s_i * G1::one(), Q_i = t_i * G2::one() on the engine's own scalar-mul kernels."""
+    import torch
+    from substrate_bn import synth
+    P = torch.empty((n, 12), dtype=torch.int64, device=dev)
+    Q = torch.empty((n, 24), dtype=torch.int64, device=dev)
+    if seed_g1 is not None:
+        g1 = torch.from_numpy(np.tile(synth.g1_one_image().view(np.int64), (n, 1))).to(dev)
+        s_img = torch.from_numpy(fr_images(n, seed_g1).view(np.int64)).to(dev)
+        ctx.g1_mul_many_dev(g1.data_ptr(), s_img.data_ptr(), n, P.data_ptr(), sh)
+    if seed_g2 is not None:
+        g2 = torch.from_numpy(np.tile(synth.g2_one_image().view(np.int64), (n, 1))).to(dev)
+        t_img = torch.from_numpy(fr_images(n, seed_g2).view(np.int64)).to(dev)
+        ctx.g2_mul_many_dev(g2.data_ptr(), t_img.data_ptr(), n, Q.data_ptr(), sh)
+    torch.cuda.synchronize(dev)
+    return P, Q
 
 
 def cpu_baseline(p_host, q_host, gpu_out, threads):
@@ -84,7 +101,6 @@ def other_workload(args, local_rank):
     """BASELINE config 3 (batched G1 * Fr) and config 5 (pairing product), 1 GPU."""
     import torch
 
-    from oracle import oracle as O
     from substrate_bn import Context
 
     dev = torch.device("cuda", local_rank)
@@ -95,19 +111,17 @@ def other_workload(args, local_rank):
            "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)", "data": "synthetic"}
     if args.workload == "g1mul":
         n = args.pairs if args.pairs != (1 << 16) else (1 << 18)
-        base = torch.from_numpy(np.tile(O.g1_one().view(np.int64), (n, 1))).to(dev)
-        k1 = torch.from_numpy(fr_images(n, 5).view(np.int64)).to(dev)
+        P, _ = device_points(ctx, n, 5, None, dev, sh)  # random Jacobian bases
         k2 = torch.from_numpy(fr_images(n, 6).view(np.int64)).to(dev)
-        P = torch.empty((n, 12), dtype=torch.int64, device=dev)
         out = torch.empty_like(P)
-        ctx.g1_mul_many_dev(base.data_ptr(), k1.data_ptr(), n, P.data_ptr(), sh)  # random Jacobian bases
         step = lambda: ctx.g1_mul_many_dev(P.data_ptr(), k2.data_ptr(), n, out.data_ptr(), sh)  # noqa: E731
         unit = "G1 scalar muls/s"
         res["config"] = {"workload": "BASELINE config 3: batched Fr x G1 (reference double-and-add chain, "
                                      "bit-exact Jacobian output)", "muls": n}
     else:
         n = args.pairs if args.pairs != (1 << 16) else (1 << 14)
-        p, q, _, _ = O.random_pairs(n, seed=21, nthreads=min(16, os.cpu_count() or 1))
+        Pd, Qd = device_points(ctx, n, 21, 22, dev, sh)
+        p, q = Pd.cpu().numpy().view(np.uint64), Qd.cpu().numpy().view(np.uint64)
         step = lambda: ctx.pairing_batch(p, q)  # noqa: E731
         unit = "pairing-product terms/s"
         res["config"] = {"workload": "BASELINE config 5: one pairing_batch over 2^14 terms (per-term Miller "
@@ -122,6 +136,7 @@ def other_workload(args, local_rank):
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     res.update({"metric": unit, "value": n * args.steps / el, "unit": unit, "ms_per_step": el / args.steps * 1e3})
+    from oracle import oracle as O  # the checker (cpu_baseline leg)
     if args.workload == "g1mul":
         m = min(args.cpu_sample, n)
         threads = min(16, os.cpu_count() or 1)
@@ -141,9 +156,7 @@ def codec_workload(args, local_rank):
     """SURVEY 8(f) rows on 2^16 elements, inputs resident in HBM, device-pointer C ABI on torch's stream."""
     import torch
 
-    from oracle import oracle as O
-    from substrate_bn import Context
-    from tests.codec_util import compress_g2
+    from substrate_bn import Context, synth
 
     dev = torch.device("cuda", local_rank)
     ctx = Context(local_rank)
@@ -153,8 +166,9 @@ def codec_workload(args, local_rank):
     threads = min(16, os.cpu_count() or 1)
     t0 = time.perf_counter()
     if args.workload in ("g2validate", "g2decompress"):
-        _, t = O.random_scalars(n, 61)
-        aff, _ = O.g2_to_affine(O.g2_mul(O.g2_one(), t, threads))  # n distinct points of the order-r subgroup
+        _, Qd = device_points(ctx, n, None, 61, dev, sh)  # n distinct points of the order-r subgroup
+        aff = synth.g2_jacobian_to_affine(Qd.cpu().numpy().view(np.uint64))
+        del Qd
         out = torch.empty((n, 24), dtype=torch.int64, device=dev)
         st = torch.empty(n, dtype=torch.uint8, device=dev)
         if args.workload == "g2validate":
@@ -166,17 +180,20 @@ def codec_workload(args, local_rank):
             wl = "AffineG2::new on 2^16 affine points (curve equation + order check [r]P == 0), mod.rs:95-113"
             ref_fn = lambda m: O.g2_affine_new(aff[:m, :8], aff[:m, 8:], threads)  # noqa: E731
         else:
-            rec = compress_g2(aff)
+            rec = synth.compress_g2(aff)
             b = torch.from_numpy(rec).to(dev)
             step = lambda: ctx.g2_from_compressed_many_dev(b.data_ptr(), n, out.data_ptr(), st.data_ptr(), sh)  # noqa
             unit, kname = "G2 decompressions/s", "k_g2_from_compressed"
             wl = "G2::from_compressed on 2^16 65-byte records (Fq2 sqrt + order check), lib.rs:506-526"
             ref_fn = lambda m: O.g2_from_compressed(rec[:m], threads)  # noqa: E731
     else:
-        p, q, _, _ = O.random_pairs(1024, seed=71, nthreads=threads)
-        g = O.pairing_many(p, q, threads)
+        Pd, Qd = device_points(ctx, 1024, 71, 73, dev, sh)
+        gd = torch.empty((1024, 48), dtype=torch.int64, device=dev)
+        ctx.pairing_many_dev(Pd.data_ptr(), Qd.data_ptr(), 1024, gd.data_ptr(), sh)
+        torch.cuda.synchronize(dev)
+        g = gd.cpu().numpy().view(np.uint64)
         a = torch.from_numpy(np.ascontiguousarray(np.tile(g, (n // 1024, 1))).view(np.int64)).to(dev)
-        _, k = O.random_scalars(n, 72, lo=0)
+        k = fr_images(n, 72, lo=0)
         kt = torch.from_numpy(np.ascontiguousarray(k).view(np.int64)).to(dev)
         out = torch.empty((n, 48), dtype=torch.int64, device=dev)
         st = None
@@ -203,6 +220,7 @@ def codec_workload(args, local_rank):
            "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)", "data": "synthetic",
            "config": {"workload": wl, "elements": n},
            "kernel": {"name": kname, "per_launch_ms": kms}}
+    from oracle import oracle as O  # the checker (cpu_baseline leg)
     m = min(args.cpu_sample, n)
     g_out = out[:m].cpu().numpy().view(np.uint64)
     t0 = time.perf_counter()
@@ -245,7 +263,6 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     from substrate_bn import Context
-    from oracle import oracle as O
 
     if args.workload in ("g2validate", "g2decompress", "gtpow"):
         return codec_workload(args, local_rank)
@@ -263,18 +280,10 @@ def main():
     sh = stream.cuda_stream
 
     # ---- synthetic inputs in HBM (engine kernels; Jacobian images)
-    g1 = torch.from_numpy(np.tile(O.g1_one().view(np.int64), (n, 1))).to(dev)
-    g2 = torch.from_numpy(np.tile(O.g2_one().view(np.int64), (n, 1))).to(dev)
-    s_img = torch.from_numpy(fr_images(n, 1 + rank).view(np.int64)).to(dev)
-    t_img = torch.from_numpy(fr_images(n, 1001 + rank).view(np.int64)).to(dev)
-    P = torch.empty((n, 12), dtype=torch.int64, device=dev)
-    Q = torch.empty((n, 24), dtype=torch.int64, device=dev)
-    ctx.g1_mul_many_dev(g1.data_ptr(), s_img.data_ptr(), n, P.data_ptr(), sh)
-    ctx.g2_mul_many_dev(g2.data_ptr(), t_img.data_ptr(), n, Q.data_ptr(), sh)
+    P, Q = device_points(ctx, n, 1 + rank, 1001 + rank, dev, sh)
     out = torch.empty((n, 48), dtype=torch.int64, device=dev)
     gathered = torch.empty((world * n, 48), dtype=torch.int64, device=dev) if world > 1 else None
     torch.cuda.synchronize(dev)
-    del g1, g2, s_img, t_img
 
     def step():
         ctx.pairing_many_dev(P.data_ptr(), Q.data_ptr(), n, out.data_ptr(), sh)
