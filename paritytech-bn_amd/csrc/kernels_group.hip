@@ -1,4 +1,9 @@
 // kernels_group.hip -- batched G1/G2 scalar multiplication (mod.rs:272-292), one lane per product.
+// fq_fold reads -q*p from an LDS table (fq.h; every kernel here calls
+// fold_table_init first)
+#ifndef BN_FOLD_LDS
+#define BN_FOLD_LDS 1
+#endif
 #include "kernels.h"
 
 namespace bn {
