@@ -138,7 +138,7 @@ def other_workload(args, local_rank):
     res.update({"metric": unit, "value": n * args.steps / el, "unit": unit, "ms_per_step": el / args.steps * 1e3})
     from oracle import oracle as O  # the checker (cpu_baseline leg)
     if args.workload == "g1mul":
-        m = min(args.cpu_sample, n)
+        m = min(args.cpu_sample or 2048, n)
         threads = min(16, os.cpu_count() or 1)
         ph, kh, oh = (t[:m].cpu().numpy().view(np.uint64) for t in (P, k2, out))
         t0 = time.perf_counter()
@@ -221,7 +221,7 @@ def codec_workload(args, local_rank):
            "config": {"workload": wl, "elements": n},
            "kernel": {"name": kname, "per_launch_ms": kms}}
     from oracle import oracle as O  # the checker (cpu_baseline leg)
-    m = min(args.cpu_sample, n)
+    m = min(args.cpu_sample or 2048, n)
     g_out = out[:m].cpu().numpy().view(np.uint64)
     t0 = time.perf_counter()
     ref, rst = ref_fn(m)
@@ -239,7 +239,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=1 << 16, help="pairings per GPU per step")
-    ap.add_argument("--cpu-sample", type=int, default=2048)
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="oracle sample size (default: 16384 pairings, 2048 for the 8(f) workloads; ~10-30 s of CPU-thread work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="pairing",
                     choices=["pairing", "g1mul", "product", "g2validate", "g2decompress", "gtpow"],
@@ -341,7 +342,7 @@ def main():
         "roofline": roofline,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        m = min(args.cpu_sample, n)
+        m = min(args.cpu_sample or 16384, n)
         threads = min(16, os.cpu_count() or 1)
         p_h = P[:m].cpu().numpy().view(np.uint64)
         q_h = Q[:m].cpu().numpy().view(np.uint64)
