@@ -112,6 +112,21 @@ def test_zero_points(ctx, pairs):
     assert np.array_equal(ctx.pairing_many(p2, q2), O.pairing_many(p2, q2))
 
 
+@pytest.mark.parametrize("n", [1, 63, 65, 129, 255])
+def test_pairing_many_ragged(ctx, pairs, n):
+    """Batch sizes that leave a partial wave / workgroup, with zero points in the tail lanes."""
+    p, q = pairs
+    p2, q2 = p[:n].copy(), q[:n].copy()
+    one = O.canon_to_mont_array([1])
+    p2[n - 1] = 0
+    p2[n - 1, 4:8] = one             # G1::zero() in the last lane
+    if n > 2:
+        q2[n - 2] = 0
+        q2[n - 2, 8:12] = one        # G2::zero() in the lane before it
+    assert np.array_equal(ctx.pairing_many(p2, q2), O.pairing_many(p2, q2, NT))
+    assert np.array_equal(ctx.pairing_batch(p2, q2), O.pairing_batch(p2, q2))
+
+
 @pytest.mark.parametrize("n", [0, 1, 5, 64])
 def test_pairing_batch(ctx, pairs, n):
     p, q = pairs
