@@ -785,7 +785,10 @@ int bn_g2_from_compressed_many_dev(bn_ctx* c, const uint8_t* d_b, size_t n, bn_g
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
-// Gt::pow: the per-lane window table lives in the context's Fq12 slots (16 of kFeSlots)
+// Gt::pow: the per-lane window table lives in the context's Fq12 slots (16 of kFeSlots);
+// k_gt_pow addresses a lane's entry by a 32-bit buffer offset (ld_fq12_buf_sel)
+static_assert(16ull * kSlotWords * kChunk * 4 + (size_t)kSlotWords * kChunk * 4 < (1ull << 31),
+              "k_gt_pow window-table offsets must fit the buffer descriptor's 31-bit range");
 int bn_gt_pow_many_dev(bn_ctx* c, const bn_gt* d_a, const bn_fr* d_k, size_t n, bn_gt* d_out, void* stream) {
     CTX_GUARD(c);
     if (n == 0) return BN_OK;

@@ -314,6 +314,23 @@ BN_INLINE auto fq_half(const Fq<K>& a_in) {
 #ifndef BN_FOLD_LDS
 #define BN_FOLD_LDS 0
 #endif
+// Diagnostic build (-DBN_DEVICE_CHECKS=1, `make -C paritytech-bn_amd dbg`):
+// every device fold counts the lanes whose quotient estimate exceeds the
+// static bound of its input (q <= kv(B) <= kMaxBound is what makes the LDS
+// table index and the subtraction safe); kernels.h exports the per-TU counter
+// as bn_dbg_fold_bad_<tu>(), read by tools/fold_check.py.
+#ifndef BN_DEVICE_CHECKS
+#define BN_DEVICE_CHECKS 0
+#endif
+#if BN_DEVICE_CHECKS && defined(__HIPCC__)
+static __device__ unsigned g_fold_bad;
+#define BN_FOLD_CHECK(q, B)                                                          \
+    do {                                                                             \
+        if ((q) > (uint32_t)kv(B)) atomicAdd(&g_fold_bad, 1u);                       \
+    } while (0)
+#else
+#define BN_FOLD_CHECK(q, B) ((void)0)
+#endif
 #if BN_FOLD_LDS
 constexpr int kFoldQ = kMaxBound + 1;  // q <= x8 * 2^232/p < 161
 constexpr int kFoldStride = 12;        // words per entry: 16-byte aligned rows
@@ -341,6 +358,9 @@ template <int B>
 __device__ __forceinline__ FoldEnt fold_fetch(const Fq<B>& x) {
     static_assert(kl(B) <= 6, "fold_fetch: normalize first");
     const uint32_t q = (uint32_t)((float)x.v[8] * 3.1531629e-07f);  // as fq_fold
+#if defined(__HIP_DEVICE_COMPILE__)
+    BN_FOLD_CHECK(q, B);
+#endif
     const uint32_t* e = g_fold_tab + q * kFoldStride;
     return FoldEnt{*(const uint4*)e, *(const uint4*)(e + 4), e[8]};
 }
@@ -378,6 +398,9 @@ BN_INLINE Fq<2> fq_fold(const Fq<B>& x) {
         fprintf(stderr, "fq_fold: q = %u > bound %d\n", q, kv(B));
         abort();
     }
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+    BN_FOLD_CHECK(q, B);
 #endif
     Fq<2> r;
     int64_t carry = 0;

@@ -91,6 +91,22 @@ __device__ __forceinline__ Fq12<B> ld_fq12_buf(const uint32_t* base, size_t n, s
     return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
 }
 
+// Per-lane slot selection (Gt::pow's window table): the descriptor is built
+// from the uniform workspace base and the lane's slot goes into the VGPR
+// offset, so the resource stays wave-uniform.  A descriptor built from a
+// lane-divergent pointer makes the compiler wrap every load in a readfirstlane
+// waterfall loop whose per-lane pointer lives in VGPRs across partial-exec
+// regions; round 1's k_gt_pow faulted with an illegal address in that form
+// (DESIGN.md §3).  vo_bytes = (slot * kSlotWords * n + i) * 4 must stay below
+// 2^31 (checked by the host launcher).
+template <int B>
+__device__ __forceinline__ Fq12<B> ld_fq12_buf_sel(const uint32_t* ws, size_t n, uint32_t vo_bytes) {
+    const auto rs = slot_rsrc(ws);
+    const int vo = (int)vo_bytes;
+    auto q = [&](int k) { return Fq2<B>{ld_fq_buf<B>(rs, vo, n, 2 * k), ld_fq_buf<B>(rs, vo, n, 2 * k + 1)}; };
+    return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
+}
+
 template <int B>
 __device__ __forceinline__ Fq6<B> ld_fq6(const uint32_t* base, size_t n, size_t i, int h) {
     return {ld_fq2<B>(base, n, i, 6 * h), ld_fq2<B>(base, n, i, 6 * h + 2), ld_fq2<B>(base, n, i, 6 * h + 4)};
@@ -269,6 +285,20 @@ __device__ __forceinline__ void fr_to_canonical(const bn_fr& k, uint32_t out[8])
 
 __device__ __forceinline__ size_t lane_id() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
+
+// BN_DEVICE_CHECKS builds: export this translation unit's fold-bound
+// violation counter (fq.h) as bn_dbg_fold_bad_<tu>().
+#if BN_DEVICE_CHECKS
+#define BN_EXPORT_FOLD_CHECK(tu)                                                  \
+    extern "C" unsigned bn_dbg_fold_bad_##tu(void) {                              \
+        unsigned h = 0;                                                           \
+        if (hipMemcpyFromSymbol(&h, HIP_SYMBOL(bn::g_fold_bad), sizeof h) != hipSuccess) \
+            return 0xffffffffu;                                                   \
+        return h;                                                                 \
+    }
+#else
+#define BN_EXPORT_FOLD_CHECK(tu)
+#endif
 
 inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 

@@ -197,3 +197,5 @@ __global__ void __launch_bounds__(kBlock) k_g2_from_compressed(const uint8_t* __
 }
 
 }  // namespace bn
+
+BN_EXPORT_FOLD_CHECK(codec)

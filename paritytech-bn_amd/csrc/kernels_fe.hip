@@ -88,3 +88,5 @@ __global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ 
 }
 
 }  // namespace bn
+
+BN_EXPORT_FOLD_CHECK(fe)

@@ -37,3 +37,5 @@ __global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, 
 }
 
 }  // namespace bn
+
+BN_EXPORT_FOLD_CHECK(group)

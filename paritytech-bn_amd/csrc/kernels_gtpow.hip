@@ -7,6 +7,16 @@
 // fixed 4-bit window: a per-lane table x^0..x^15 in lane-strided HBM slots,
 // 252 generic squarings and 63 products by a table entry.  x^e is unique, so
 // the canonical output equals the reference's.
+//
+// The table entry is selected per lane through the VGPR offset of a buffer
+// descriptor built from the uniform workspace base (ld_fq12_buf_sel): the
+// descriptor itself never depends on the lane (round 1 built it from a
+// per-lane pointer, which the compiler lowers to readfirstlane waterfall loops,
+// and that build faulted once the LDS fold table was enabled).
+// fq_fold reads -q*p from the LDS table as in the other pairing-path kernels.
+#ifndef BN_FOLD_LDS
+#define BN_FOLD_LDS 1
+#endif
 #include "kernels.h"
 
 namespace bn {
@@ -24,6 +34,8 @@ __global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, 
         asm volatile("" : "+s"(nn));
         return nn;
     };
+    // byte offset of lane i's copy of table entry t (t is per lane)
+    auto sel = [&](uint32_t t, size_t nn) { return (uint32_t)(((size_t)t * kSlotWords * nn + i) * 4); };
     const Fq12<kF> x = widen<kF>(ld_gt(a[i]));
     {
         const size_t nn = stride();
@@ -42,7 +54,7 @@ __global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, 
     Fq12<kF> acc;
     {
         const size_t nn = stride();
-        acc = ld_fq12_buf<kF>(slot(e[7] >> 28, nn), nn, i);
+        acc = ld_fq12_buf_sel<kF>(ws, nn, sel(e[7] >> 28, nn));
     }
 #pragma unroll 1
     for (int w = 62; w >= 0; --w) {
@@ -52,9 +64,11 @@ __global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, 
 #pragma unroll 1
         for (int s = 0; s < 4; ++s) acc = narrow12<kF>(fq12_sqr(acc));
         const size_t nn = stride();
-        acc = mul12(acc, ld_fq12_buf<kF>(slot(e[7] >> 28, nn), nn, i));
+        acc = mul12(acc, ld_fq12_buf_sel<kF>(ws, nn, sel(e[7] >> 28, nn)));
     }
     st_gt(out[i], acc);
 }
 
 }  // namespace bn
+
+BN_EXPORT_FOLD_CHECK(gtpow)

@@ -73,3 +73,5 @@ __global__ void __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ 
 }
 
 }  // namespace bn
+
+BN_EXPORT_FOLD_CHECK(pairing)

@@ -29,3 +29,5 @@ __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict_
 }
 
 }  // namespace bn
+
+BN_EXPORT_FOLD_CHECK(util)

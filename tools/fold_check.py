@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Device-side fold-bound check (diagnostic; not a parity test).
+
+Loads libbn254mi_dbg.so (`make -C paritytech-bn_amd dbg`: every fold counts
+the lanes whose top-digit quotient estimate q exceeds the static bound of its
+input, fq.h BN_DEVICE_CHECKS), drives every kernel family over seeded inputs
+and prints the per-translation-unit violation counters as one JSON line.
+All counters 0 means no fold saw a value above the bound its type claims, so
+no LDS table index went past its 161 entries.
+
+    BN254MI_LIB=paritytech-bn_amd/libbn254mi_dbg.so python tools/fold_check.py [n]
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "paritytech-bn_amd"))
+os.environ.setdefault("BN254MI_LIB", os.path.join(ROOT, "paritytech-bn_amd", "libbn254mi_dbg.so"))
+
+from substrate_bn import _native, synth  # noqa: E402
+
+TUS = ["pairing", "fe", "group", "gtpow", "codec", "util"]
+
+
+def counters(L):
+    out = {}
+    for t in TUS:
+        fn = getattr(L, "bn_dbg_fold_bad_" + t)
+        fn.restype = ctypes.c_uint
+        out[t] = int(fn())
+    return out
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    L = _native.load()
+    ctx = _native.Context(0)
+    before = counters(L)
+    g1 = np.tile(synth.g1_one_image(), (n, 1))
+    g2 = np.tile(synth.g2_one_image(), (n, 1))
+    p = ctx.g1_mul_many(g1, synth.fr_images(n, 1))
+    q = ctx.g2_mul_many(g2, synth.fr_images(n, 2))
+    gt = ctx.pairing_many(p, q)
+    ctx.pairing_batch(p[:1024], q[:1024])
+    ctx.miller_loop_many(p[:256], q[:256])
+    ctx.gt_pow_many(gt, synth.fr_images(n, 3, lo=0))
+    for op in ("mul", "sqr", "inv", "cyc_sqr", "exp_by_neg_z", "frob1", "frob2", "frob3"):
+        ctx.fq12_op_many(op, gt[:256], gt[256:512] if op == "mul" else None)
+    aff = synth.g2_jacobian_to_affine(q[:512])
+    ctx.g2_affine_new_many(aff[:, :8], aff[:, 8:])
+    ctx.g2_from_compressed_many(synth.compress_g2(aff))
+    after = counters(L)
+    res = {"check": "device fold bound (q <= static bound) on every fold, BN_DEVICE_CHECKS build",
+           "n": n, "violations": {t: after[t] - before[t] for t in TUS}}
+    res["ok"] = all(v == 0 for v in res["violations"].values())
+    print(json.dumps(res), flush=True)
+    return 0 if res["ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
