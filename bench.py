@@ -1,26 +1,38 @@
 #!/usr/bin/env python3
-"""bench.py -- BN254 pairings/sec on MI355X (BASELINE.json metric, config 2 at N=1).
+"""bench.py -- BN254 pairings/sec on MI355X (BASELINE.json metric).
 
-One step = one pass of the hot path over one batch: `pairs` independent
-optimal-ate pairings e(P_i, Q_i) per GPU (default 2^16 = BASELINE config 2),
+One step = one pass of the hot path over one batch of synthetic pairs,
 inputs resident in HBM, through the engine's C ABI (bn_pairing_many_dev:
-to_affine + G2 line precomputation, Miller loop, final exponentiation).  With
-N > 1 GPUs each rank runs its own 2^16 pairs (weak scaling, no data-path
-collective) and the step ends with one RCCL all-gather of every rank's Gt
-results over xGMI (BASELINE config 4's exchange), so every rank holds all
-N x 2^16 results.
+to_affine + G2 line precomputation, Miller loop, final exponentiation).
 
-Synthetic inputs: P_i = s_i * G1::one(), Q_i = t_i * G2::one() with s_i, t_i
-uniform in [1, r) from a seeded SplitMix64 (seed 1 + rank), computed by the
-engine's own scalar-multiplication kernels and kept in Jacobian form (z != 1),
-exactly the reference's `G * Fr` output images.
+  N = 1  (default): BASELINE config 2 -- 2^16 independent pairings on one GPU.
+  N > 1  (default): BASELINE config 4 -- 2^20 pairings sharded contiguously
+         over the N ranks (2^20/N each, strong scaling); every step ends with
+         an RCCL all-gather of all 2^20 Gt results over xGMI, issued per 2^16
+         chunk on RCCL's stream so it overlaps the next chunk's kernels.
+         `--config 2` keeps 2^16 pairs per rank instead (weak scaling).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs n]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment
+starts `torch.distributed.run` with N ranks as a child process (before this
+process touches a GPU) and exits with its status; under a launcher the world
+size must equal --gpus.
+
+Synthetic inputs: row j of a global dataset is P_j = s_j * G1::one(),
+Q_j = t_j * G2::one(); s_j, t_j are Montgomery Fr images uniform in [1, r)
+from SplitMix64 seeds fixed per 4096-row block (substrate_bn/synth.py), so
+every rank builds exactly its rows and any rank can rebuild any other rank's.
+The points come from the engine's own scalar-multiplication kernels, kept in
+Jacobian form (z != 1) -- exactly the reference's `G * Fr` output images.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4]
+    python bench.py --workload g1mul|product|g2validate|g2decompress|gtpow
+    python bench.py --gpus 2 --dry-run-cpu   # control flow on CPU (gloo, stub engine)
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,13 +42,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "paritytech-bn_amd"))
 sys.path.insert(0, ROOT)
 
-# Algorithmic work per pairing in generic Fq Montgomery products (SURVEY.md §8(d),
-# Appendix B: reference formulas with x(-1) and x xi folded into adds, inversions
-# excluded), per kernel phase of bn_pairing_many_dev.
-# k_fq12_vm: the reference's 8767 less what the width-4 signed-window chains for u
-# save per exp_by_neg_z (16 Fq12 products instead of 27, one extra cyclotomic
-# square of 18): the work counted is the work the kernel does.
-FQMUL_PER_PAIRING = {"k_prepare": 19 + 2655, "k_miller": 6045, "k_fq12_vm": 8767 - 3 * (11 * 54 - 18), "k_fe_out": 0}
+# Algorithmic work per pairing in generic Fq Montgomery products, per kernel
+# phase of bn_pairing_many_dev: SURVEY.md §8(d) / Appendix B (the reference's
+# formulas with x(-1) and x xi folded into adds, inversions excluded):
+# to_affine 19 + precompute 2,655, Miller loop 6,045, final exponentiation 8,767.
+# (The engine's FE runs windowed exp_by_neg_z chains that do less work than the
+# reference's binary chains; the roofline credits only the reference count.)
+FQMUL_PER_PAIRING = {"k_prepare": 19 + 2655, "k_miller": 6045, "k_fq12_vm": 8767, "k_fe_out": 0}
+FQMUL_BASIS = "SURVEY.md 8(d): reference Fq-mul counts (FE 8767, Miller 6045, prepare 2674), x128 MAD32 each"
 MAD32_PER_FQMUL = 128  # one 8x32-bit CIOS product: 64 (a*b) + 64 (m*p) v_mad_u64_u32
 # gfx950 integer-VALU peak for v_mad_u64_u32: 4 cycles per wave64 instruction (measured,
 # tools/ubench.hip) = 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  ubench sustains 34.7 T/s.
@@ -71,19 +84,69 @@ def device_points(ctx, n, seed_g1, seed_g2, dev, sh):
     return P, Q
 
 
-def cpu_baseline(p_host, q_host, gpu_out, threads):
-    """Oracle (C restatement of the reference CPU path) on a bounded sample."""
+def host_cpus():
+    """The CPUs this process may use (affinity set, capped by a cgroup CPU quota)
+    and the host CPU model.  On the GPU box os.cpu_count() shows the whole
+    machine while the job's share is a quota, so the quota sets the thread count."""
+    info = {"model": None, "visible": os.cpu_count()}
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    info["affinity"] = aff
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as fh:
+                f = fh.read().split()
+        except OSError:
+            continue
+        if path.endswith("cpu.max") and f and f[0] != "max":
+            quota = int(f[0]) / int(f[1])
+        elif path.endswith("quota_us") and f and int(f[0]) > 0:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                quota = int(f[0]) / int(fh.read())
+        break
+    info["cgroup_cpu_quota"] = quota
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    # the pool's stated share for one GPU is 16 CPUs (OMP_NUM_THREADS etc. are set to it)
+    env_cap = os.environ.get("OMP_NUM_THREADS")
+    if env_cap and env_cap.isdigit() and quota is None and aff > int(env_cap):
+        usable = int(env_cap)
+        info["capped_by"] = "OMP_NUM_THREADS (the box's per-GPU CPU share)"
+    info["usable"] = usable
+    return info
+
+
+def cpu_baseline(p_host, q_host, gpu_out, cpus, single_sample=1024):
+    """Oracle (C restatement of the reference CPU path) on a bounded sample:
+    all usable cores (one pairing per thread) and one core."""
     from oracle import oracle as O
     n = p_host.shape[0]
+    threads = cpus["usable"]
     O.pairing_many(p_host[:16], q_host[:16], threads)  # warm
     t0 = time.perf_counter()
     ref = O.pairing_many(p_host, q_host, threads)
     dt = time.perf_counter() - t0
+    m1 = min(single_sample, n)
+    t0 = time.perf_counter()
+    ref1 = O.pairing_many(p_host[:m1], q_host[:m1], 1)
+    dt1 = time.perf_counter() - t0
     return {"value": n / dt, "unit": "pairings/s", "cores": threads, "kind": "port",
+            "single_core": {"value": m1 / dt1, "unit": "pairings/s", "sample": "%d pairings, 1 thread" % m1},
+            "cpu_model": cpus["model"], "cpus_visible": cpus["visible"], "cpus_usable": threads,
             "sample": "%d pairings of the bench's own inputs, oracle/bn_oracle.c (C restatement of substrate-bn "
-                      "0.6.0: u128-digit Montgomery, binary-EEA inverse, same formulas), %d threads, %.2f s wall"
-                      % (n, threads, dt),
-            "parity_sample_bit_exact": bool(np.array_equal(ref, gpu_out))}
+                      "0.6.0: u128-digit Montgomery, binary-EEA inverse, same formulas), %d threads (one pairing "
+                      "per thread), %.2f s wall" % (n, threads, dt),
+            "parity_sample_bit_exact": bool(np.array_equal(ref, gpu_out) and np.array_equal(ref1, gpu_out[:m1]))}
 
 
 def pmc_traffic(kernel):
@@ -139,7 +202,7 @@ def other_workload(args, local_rank):
     from oracle import oracle as O  # the checker (cpu_baseline leg)
     if args.workload == "g1mul":
         m = min(args.cpu_sample or 2048, n)
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_cpus()["usable"]
         ph, kh, oh = (t[:m].cpu().numpy().view(np.uint64) for t in (P, k2, out))
         t0 = time.perf_counter()
         ref = O.g1_mul(ph, kh, threads)
@@ -163,7 +226,7 @@ def codec_workload(args, local_rank):
     stream = torch.cuda.Stream(dev)  # a real stream: handle 0 would mean the context's own stream
     sh = stream.cuda_stream
     n = args.pairs
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cpus()["usable"]
     t0 = time.perf_counter()
     if args.workload in ("g2validate", "g2decompress"):
         _, Qd = device_points(ctx, n, None, 61, dev, sh)  # n distinct points of the order-r subgroup
@@ -233,127 +296,292 @@ def codec_workload(args, local_rank):
     print(json.dumps(res), flush=True)
 
 
+# ============================================================== pairing workload (configs 2 and 4)
+class GpuEngine:
+    """The product path: the engine's C ABI on one MI355X, all work on one real HIP stream."""
+    dry = False
+
+    def __init__(self, local_rank):
+        import torch
+        from substrate_bn import Context
+        self.torch = torch
+        self.dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(self.dev)
+        self.ctx = Context(local_rank)
+        # one real (non-default) stream for the kernels, torch's copies and the
+        # collectives' ordering (handle 0 would mean the context's own stream)
+        self.stream = torch.cuda.Stream(self.dev)
+        torch.cuda.set_stream(self.stream)
+        self.sh = self.stream.cuda_stream
+
+    def points(self, lo, n):
+        """P, Q (device, Jacobian images) for global dataset rows [lo, lo + n)."""
+        from substrate_bn import synth
+        torch = self.torch
+        s, t = synth.dataset_scalars(lo, n)
+        P = torch.empty((n, 12), dtype=torch.int64, device=self.dev)
+        Q = torch.empty((n, 24), dtype=torch.int64, device=self.dev)
+        g1 = torch.from_numpy(np.tile(synth.g1_one_image().view(np.int64), (n, 1))).to(self.dev)
+        g2 = torch.from_numpy(np.tile(synth.g2_one_image().view(np.int64), (n, 1))).to(self.dev)
+        s_d = torch.from_numpy(s.view(np.int64)).to(self.dev)
+        t_d = torch.from_numpy(t.view(np.int64)).to(self.dev)
+        self.ctx.g1_mul_many_dev(g1.data_ptr(), s_d.data_ptr(), n, P.data_ptr(), self.sh)
+        self.ctx.g2_mul_many_dev(g2.data_ptr(), t_d.data_ptr(), n, Q.data_ptr(), self.sh)
+        self.sync()
+        return P, Q
+
+    def empty_gt(self, n):
+        return self.torch.empty((n, 48), dtype=self.torch.int64, device=self.dev)
+
+    def pairing(self, P, Q, out):
+        self.ctx.pairing_many_dev(P.data_ptr(), Q.data_ptr(), P.shape[0], out.data_ptr(), self.sh)
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.dev)
+
+    @staticmethod
+    def host(t):
+        return t.cpu().numpy().view(np.uint64)
+
+
+class DryEngine:
+    """--dry-run-cpu only: exercises bench.py's launch, sharding, all-gather,
+    timing and cross-rank check on CPU tensors with gloo.  pairing() is a
+    deterministic row mix, NOT a pairing; the JSON line says "dry_run": true."""
+    dry = True
+
+    def __init__(self, local_rank):
+        import torch
+        self.torch = torch
+
+    def points(self, lo, n):
+        from substrate_bn import synth
+        s, t = synth.dataset_scalars(lo, n)
+        P = self.torch.from_numpy(np.ascontiguousarray(np.tile(s, (1, 3))).view(np.int64))
+        Q = self.torch.from_numpy(np.ascontiguousarray(np.tile(t, (1, 6))).view(np.int64))
+        return P, Q
+
+    def empty_gt(self, n):
+        return self.torch.empty((n, 48), dtype=self.torch.int64)
+
+    def pairing(self, P, Q, out):
+        out[:, :12] = P
+        out[:, 12:36] = Q
+        out[:, 36:] = P ^ Q[:, :12]
+
+    def sync(self):
+        pass
+
+    @staticmethod
+    def host(t):
+        return t.numpy().view(np.uint64)
+
+
+def run_pairing(args, eng, rank, world, dist):
+    torch = eng.torch
+    if args.config == 4:
+        total = args.total
+        if total % world:
+            raise SystemExit("config 4: --total %d is not divisible by the world size %d" % (total, world))
+        local_n = total // world
+        scaling = "strong"
+        wl = ("BASELINE config 4: %d pairings sharded contiguously over %d GPU(s) (%d each) + RCCL all-gather "
+              "of all Gt results over xGMI inside the step" % (total, world, local_n)) if world > 1 else \
+             ("BASELINE config 4 workload on 1 GPU: %d independent pairings (no exchange)" % total)
+    else:
+        local_n = args.pairs
+        total = local_n * world
+        scaling = "weak"
+        wl = "BASELINE config 2: %d independent pairings e(P_i,Q_i) per GPU" % local_n + \
+             (" + RCCL all-gather of Gt" if world > 1 else "")
+    lo = rank * local_n
+    t0 = time.perf_counter()
+    P, Q = eng.points(lo, local_n)
+    out = eng.empty_gt(local_n)
+    gathered = eng.empty_gt(total) if world > 1 else None
+    eng.sync()
+    log("rank %d: %d pairs ready in %.1f s" % (rank, local_n, time.perf_counter() - t0))
+    chunk = min(local_n, args.chunk)
+    bounds = [(c0, min(c0 + chunk, local_n)) for c0 in range(0, local_n, chunk)]
+
+    def step():
+        works = []
+        for c0, c1 in bounds:
+            eng.pairing(P[c0:c1], Q[c0:c1], out[c0:c1])
+            if world > 1:  # overlaps the next chunk's kernels (RCCL's own stream waits on this one)
+                outs = [gathered[r * local_n + c0:r * local_n + c1] for r in range(world)]
+                works.append(dist.all_gather(outs, out[c0:c1], async_op=True))
+        for w in works:
+            w.wait()
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    gpu = not eng.dry
+    if gpu:
+        eng.ctx.phase_times()  # discard
+        eng.ctx.set_phase_timing(True)
+    if world > 1:
+        dist.barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if gpu:
+        eng.ctx.set_phase_timing(False)
+        phase_ms, launches = eng.ctx.phase_times()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=getattr(eng, "dev", "cpu"))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = total * args.steps / elapsed
+
+    res = {
+        "metric": "BN254 pairings/sec (batched) at 1/2/4/8 MI355X; bit-exact vs CPU ref",
+        "value": value, "unit": "pairings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": scaling,
+        "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)",
+        "data": "synthetic: P_j = s_j*G1::one(), Q_j = t_j*G2::one(), s,t uniform Fr images in [1,r), "
+                "SplitMix64 seeds per 4096-row block (substrate_bn/synth.py dataset_scalars)",
+        "config": {"workload": wl, "total_pairs": total, "pairs_per_gpu": local_n, "parallelism": "dp%d" % world,
+                   "chunk": chunk, "allgather_in_step": world > 1, "inputs": "HBM-resident Jacobian images",
+                   "hbm_io_bytes_per_pairing": 96 + 192 + 384},
+    }
+    if eng.dry:
+        res["dry_run"] = True
+        res["dtype"] = "n/a (dry run: stub engine on CPU, not a pairing)"
+    if gpu:
+        per_launch_ms = {PHASES[k]: phase_ms[k] / max(launches, 1) for k in range(4)}
+        dom = max(per_launch_ms, key=per_launch_ms.get)
+        achieved = FQMUL_PER_PAIRING[dom] * MAD32_PER_FQMUL * chunk / (per_launch_ms[dom] * 1e-3)
+        res["roofline"] = {
+            "bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
+            "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)", "frac": achieved / PEAK_MAD32_PER_S,
+            "traffic": pmc_traffic(dom), "kernel": dom, "pairs_per_launch": chunk, "basis": FQMUL_BASIS,
+            "per_launch_ms": {k: round(v, 4) for k, v in per_launch_ms.items()},
+            "whole_pairing_frac": value / world * sum(FQMUL_PER_PAIRING.values()) * MAD32_PER_FQMUL
+            / PEAK_MAD32_PER_S}
+
+    # cross-rank equality: rebuild a sample of the next rank's rows here and compare
+    # this GPU's results with what the all-gather delivered
+    if world > 1:
+        src = (rank + 1) % world
+        m = min(128, local_n)
+        mism = 0
+        for j0 in sorted({0, local_n - m}):
+            Pc, Qc = eng.points(src * local_n + j0, m)
+            oc = eng.empty_gt(m)
+            eng.pairing(Pc, Qc, oc)
+            eng.sync()
+            got = eng.host(gathered[src * local_n + j0:src * local_n + j0 + m])
+            mism += int((eng.host(oc) != got).any(axis=1).sum())
+        cnt = torch.tensor([mism, 1 if mism == 0 else 0], dtype=torch.int64, device=getattr(eng, "dev", "cpu"))
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+        res["cross_rank_check"] = {"rows_per_rank": m * len({0, local_n - m}), "mismatches": int(cnt[0]),
+                                   "ranks_ok": int(cnt[1]),
+                                   "what": "each rank recomputes rows of the next rank's shard on its own GPU "
+                                           "and compares them with the all-gathered Gt"}
+
+    if rank == 0 and world == 1 and gpu and not args.no_cpu_baseline:
+        m = min(args.cpu_sample or 16384, local_n)
+        p_h, q_h, o_h = (eng.host(t[:m]) for t in (P, Q, out))
+        res["cpu_baseline"] = cpu_baseline(p_h, q_h, o_h, host_cpus())
+    if rank == 0 and world == 1 and gpu and not args.no_e2e:
+        # host buffers through bn_pairing_many: H2D + kernels + D2H (PCIe-inclusive, not `value`)
+        p_h, q_h = eng.host(P), eng.host(Q)
+        eng.ctx.pairing_many(p_h[:1024], q_h[:1024])
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            o_h = eng.ctx.pairing_many(p_h, q_h)
+        dt = (time.perf_counter() - t0) / reps
+        res["host_buffer_e2e"] = {"value": local_n / dt, "unit": "pairings/s", "ms_per_call": dt * 1e3,
+                                  "what": "bn_pairing_many on pageable host buffers (H2D + kernels + D2H)",
+                                  "matches_hbm_path": bool(np.array_equal(o_h, eng.host(out)))}
+    return res
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 without a launcher: run torch.distributed.run with N ranks as a
+    child (this process never touches a GPU) and return its exit status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench: launching %d ranks: %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=1 << 16, help="pairings per GPU per step")
+    ap.add_argument("--config", type=int, choices=[2, 4], default=None,
+                    help="2: 2^16 pairs per GPU (weak scaling); 4: --total pairs sharded over the GPUs "
+                         "(strong scaling, all-gather in the step). Default: 2 on one GPU, 4 on several.")
+    ap.add_argument("--pairs", type=int, default=1 << 16, help="config 2: pairings per GPU per step")
+    ap.add_argument("--total", type=int, default=1 << 20, help="config 4: pairings per step over all GPUs")
+    ap.add_argument("--chunk", type=int, default=1 << 16,
+                    help="pairings per launch set (2^16 = one wave per SIMD); all-gathers go per chunk")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="oracle sample size (default: 16384 pairings, 2048 for the 8(f) workloads; ~10-30 s of CPU-thread work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) figure")
+    ap.add_argument("--dry-run-cpu", action="store_true",
+                    help="control-flow check on CPU: gloo + a stub engine (no pairing is computed)")
     ap.add_argument("--workload", default="pairing",
                     choices=["pairing", "g1mul", "product", "g2validate", "g2decompress", "gtpow"],
-                    help="pairing: config 2 (default); g1mul: config 3 (2^18 G1*Fr); product: config 5 "
+                    help="pairing: configs 2/4 (default); g1mul: config 3 (2^18 G1*Fr); product: config 5 "
                          "(2^14-term pairing_batch); SURVEY 8(f): g2validate (AffineG2::new incl. the order "
                          "check), g2decompress (G2::from_compressed), gtpow (Gt::pow(Fr)), 2^16 each")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = 2 if args.gpus == 1 else 4
+
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        return spawn_ranks(args)
+    world = int(world_env or 1)
+    if world != args.gpus:
+        log("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.workload != "pairing":
+        if world > 1:
+            log("bench: --workload %s runs on one GPU" % args.workload)
+            return 2
+        if args.workload in ("g2validate", "g2decompress", "gtpow"):
+            codec_workload(args, local_rank)
+        else:
+            other_workload(args, local_rank)
+        return 0
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    eng = (DryEngine if args.dry_run_cpu else GpuEngine)(local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-
-    from substrate_bn import Context
-
-    if args.workload in ("g2validate", "g2decompress", "gtpow"):
-        return codec_workload(args, local_rank)
-    if args.workload != "pairing":
-        return other_workload(args, local_rank)
-
-    n = args.pairs
-    ctx = Context(local_rank)
-    ctx.reserve(n)
-    # One real (non-default) stream for the engine's kernels, torch's copies and the
-    # RCCL all-gather, so the collective is ordered after the pairings it gathers
-    # (handle 0 would send the kernels to the context's own non-blocking stream).
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    sh = stream.cuda_stream
-
-    # ---- synthetic inputs in HBM (engine kernels; Jacobian images)
-    P, Q = device_points(ctx, n, 1 + rank, 1001 + rank, dev, sh)
-    out = torch.empty((n, 48), dtype=torch.int64, device=dev)
-    gathered = torch.empty((world * n, 48), dtype=torch.int64, device=dev) if world > 1 else None
-    torch.cuda.synchronize(dev)
-
-    def step():
-        ctx.pairing_many_dev(P.data_ptr(), Q.data_ptr(), n, out.data_ptr(), sh)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    ctx.phase_times()  # discard
-
-    ctx.set_phase_timing(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ctx.set_phase_timing(False)
-    phase_ms, launches = ctx.phase_times()
-
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    total = n * world * args.steps
-    value = total / elapsed
-    # dominant kernel: largest share of device time
-    per_launch_ms = {PHASES[k]: phase_ms[k] / max(launches, 1) for k in range(4)}
-    dom = max(per_launch_ms, key=per_launch_ms.get)
-    mad_per_launch = FQMUL_PER_PAIRING[dom] * MAD32_PER_FQMUL * n
-    achieved = mad_per_launch / (per_launch_ms[dom] * 1e-3)
-    roofline = {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
-                "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)", "frac": achieved / PEAK_MAD32_PER_S,
-                "traffic": pmc_traffic(dom), "kernel": dom,
-                "per_launch_ms": {k: round(v, 4) for k, v in per_launch_ms.items()},
-                "whole_pairing_frac": value / world * sum(FQMUL_PER_PAIRING.values()) * MAD32_PER_FQMUL
-                / PEAK_MAD32_PER_S}
-
-    res = {
-        "metric": "BN254 pairings/sec (batched) at 1/2/4/8 MI355X; bit-exact vs CPU ref",
-        "value": value, "unit": "pairings/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)",
-        "data": "synthetic: P_i = s_i*G1::one(), Q_i = t_i*G2::one(), s,t uniform in [1,r), SplitMix64 seed 1+rank",
-        "config": {"workload": "BASELINE config 2: 2^16 independent pairings e(P_i,Q_i) per GPU"
-                               + (" + RCCL all-gather of Gt (config 4 exchange)" if world > 1 else ""),
-                   "pairs_per_gpu": n, "parallelism": "dp%d" % world, "inputs": "HBM-resident Jacobian images",
-                   "hbm_io_bytes_per_pairing": 96 + 192 + 384},
-        "roofline": roofline,
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        m = min(args.cpu_sample or 16384, n)
-        threads = min(16, os.cpu_count() or 1)
-        p_h = P[:m].cpu().numpy().view(np.uint64)
-        q_h = Q[:m].cpu().numpy().view(np.uint64)
-        o_h = out[:m].cpu().numpy().view(np.uint64)
-        res["cpu_baseline"] = cpu_baseline(p_h, q_h, o_h, threads)
+        if eng.dry:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    res = run_pairing(args, eng, rank, world, dist)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -37,6 +37,14 @@ struct bn_ctx {
     // staging for host-buffer calls (device)
     size_t stage_bytes = 0;
     void* stage = nullptr;
+    // The workspace (coeffs, paff, slots, flags, d_err, stage) is shared by every
+    // call on this context.  Host-side, the mutex serializes the calls; device-side,
+    // every workspace user records ws_event on its stream when it has enqueued its
+    // work, and the next user's stream waits on that event first (WsUse), so _dev
+    // calls on different caller streams run in call order instead of racing on the
+    // same buffers.  No caller stream is remembered past its call.
+    hipEvent_t ws_event = nullptr;
+    bool ws_pending = false;
 };
 
 namespace {
@@ -51,6 +59,26 @@ int fail(bn_ctx* c, int code, const std::string& msg) {
         if (e_ != hipSuccess)                                                            \
             return fail(ctx, BN_ERR_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
     } while (0)
+
+// order this call's device work after the workspace's previous user (see bn_ctx)
+int ws_acquire(bn_ctx* c, hipStream_t s) {
+    if (c->ws_pending) HIPCHK(c, hipStreamWaitEvent(s, c->ws_event, 0));
+    return BN_OK;
+}
+// ... and mark this call's work as the workspace's latest user (scope exit)
+struct WsUse {
+    bn_ctx* c;
+    hipStream_t s;
+    ~WsUse() {
+        if (hipEventRecord(c->ws_event, s) == hipSuccess) c->ws_pending = true;
+    }
+};
+// before freeing workspace buffers: wait until no queued work can still read them
+int ws_drain(bn_ctx* c) {
+    if (c->ws_pending) HIPCHK(c, hipEventSynchronize(c->ws_event));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return BN_OK;
+}
 
 constexpr int kFeSlots = 32;  // slot 0: Miller value, 1: easy-part result, 2..: temporaries
 
@@ -198,10 +226,14 @@ uint32_t build_final_exp(Prog& P) {
 int reserve(bn_ctx* c, size_t n) {
     if (n <= c->cap) return BN_OK;
     n = n < 1024 ? 1024 : n;
-    if (c->coeffs) hipFree(c->coeffs);
-    if (c->paff) hipFree(c->paff);
-    if (c->slots) hipFree(c->slots);
-    if (c->flags) hipFree(c->flags);
+    if (c->cap) {
+        int r = ws_drain(c);
+        if (r) return r;
+    }
+    if (c->coeffs) HIPCHK(c, hipFree(c->coeffs));
+    if (c->paff) HIPCHK(c, hipFree(c->paff));
+    if (c->slots) HIPCHK(c, hipFree(c->slots));
+    if (c->flags) HIPCHK(c, hipFree(c->flags));
     c->coeffs = nullptr; c->paff = nullptr; c->slots = nullptr; c->flags = nullptr; c->cap = 0;
     HIPCHK(c, hipMalloc(&c->coeffs, n * (size_t)kCoeffFq * 9 * 4));
     HIPCHK(c, hipMalloc(&c->paff, n * 2 * 9 * 4));
@@ -212,7 +244,11 @@ int reserve(bn_ctx* c, size_t n) {
 }
 int stage(bn_ctx* c, size_t bytes) {
     if (bytes <= c->stage_bytes) return BN_OK;
-    if (c->stage) hipFree(c->stage);
+    if (c->stage) {
+        int r = ws_drain(c);
+        if (r) return r;
+        HIPCHK(c, hipFree(c->stage));
+    }
     c->stage = nullptr;
     c->stage_bytes = 0;
     HIPCHK(c, hipMalloc(&c->stage, bytes));
@@ -272,10 +308,16 @@ int clear_err(bn_ctx* c, hipStream_t s) {
         int r_ = (x);          \
         if (r_) return r_;     \
     } while (0)
+// host-buffer entry points: the lock for the whole call, and the context stream
+// ordered after the workspace's previous user
+#define CTX_GUARD_HOST(ctx)                \
+    CTX_GUARD(ctx);                        \
+    RET_IF(ws_acquire((ctx), (ctx)->stream)); \
+    WsUse ws_use_{(ctx), (ctx)->stream}
 
 template <typename P, typename K>
 static int host_mul(bn_ctx* c, const P* p, const bn_fr* k, size_t n, P* out, K kernel) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     if (n == 0) return BN_OK;
     if (!p || !k || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     RET_IF(stage(c, n * (2 * sizeof(P) + sizeof(bn_fr))));
@@ -353,6 +395,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
         return BN_ERR_INVALID_ARGUMENT;
     }
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess ||
         hipMalloc(&c->d_prog, P.s.size() * 4) != hipSuccess ||
         hipMemcpy(c->d_prog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -365,8 +408,10 @@ int bn_ctx_create(int device, bn_ctx** out) {
 
 int bn_ctx_destroy(bn_ctx* c) {
     if (!c) return BN_ERR_INVALID_ARGUMENT;
-    hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
+    (void)hipSetDevice(c->device);
+    if (c->ws_pending) (void)hipEventSynchronize(c->ws_event);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->ws_event) (void)hipEventDestroy(c->ws_event);
     for (void* p : {(void*)c->coeffs, (void*)c->paff, (void*)c->slots, (void*)c->flags, (void*)c->d_err,
                     (void*)c->d_prog, c->stage})
         if (p) hipFree(p);
@@ -399,12 +444,14 @@ static hipEvent_t take_event(bn_ctx* c) {
     return e;
 }
 
-int bn_pairing_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, void* stream) {
-    CTX_GUARD(c);
+// n pairings of device arrays on stream s; the caller holds the lock
+static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out,
+                                 hipStream_t s) {
     if (n == 0) return BN_OK;
     if (!d_p || !d_q || !d_out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
-    hipStream_t s = pick(c, stream);
     RET_IF(reserve(c, n < kChunk ? n : kChunk));
+    RET_IF(ws_acquire(c, s));
+    WsUse use{c, s};
     for (size_t off = 0; off < n; off += kChunk) {
         const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
         std::array<hipEvent_t, 5> ev{};
@@ -426,6 +473,11 @@ int bn_pairing_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n,
         if (c->timing) c->ev_marks.push_back(ev);
     }
     return BN_OK;
+}
+
+int bn_pairing_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, void* stream) {
+    CTX_GUARD(c);
+    return pairing_many_dev_impl(c, d_p, d_q, n, d_out, pick(c, stream));
 }
 
 int bn_set_phase_timing(bn_ctx* c, int enable) {
@@ -457,26 +509,19 @@ int bn_get_phase_times(bn_ctx* c, float* ms, int* launches) {
 }
 
 int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
-    if (!c) return BN_ERR_INVALID_ARGUMENT;
+    CTX_GUARD_HOST(c);  // held for the whole call: staging, kernels, readback
     if (n == 0) return BN_OK;
     if (!p || !q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     for (size_t off = 0; off < n; off += kChunk) {
         const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
-        bn_g1* dp;
-        bn_g2* dq;
-        bn_gt* dout;
-        {
-            CTX_GUARD(c);
-            RET_IF(stage(c, m * (sizeof(bn_g1) + sizeof(bn_g2) + sizeof(bn_gt))));
-            dp = (bn_g1*)c->stage;
-            dq = (bn_g2*)(dp + m);
-            dout = (bn_gt*)(dq + m);
-            RET_IF(clear_err(c, c->stream));
-            HIPCHK(c, hipMemcpyAsync(dp, p + off, m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
-            HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
-        }
-        RET_IF(bn_pairing_many_dev(c, dp, dq, m, dout, nullptr));
-        CTX_GUARD(c);
+        RET_IF(stage(c, m * (sizeof(bn_g1) + sizeof(bn_g2) + sizeof(bn_gt))));
+        bn_g1* dp = (bn_g1*)c->stage;
+        bn_g2* dq = (bn_g2*)(dp + m);
+        bn_gt* dout = (bn_gt*)(dq + m);
+        RET_IF(clear_err(c, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dp, p + off, m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
+        RET_IF(pairing_many_dev_impl(c, dp, dq, m, dout, c->stream));
         HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
         int bits = 0;
         RET_IF(check_err(c, c->stream, &bits));
@@ -562,7 +607,7 @@ static int final_exp_host(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8
 }
 
 int bn_pairing_batch(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     if (!out || (n && (!p || !q))) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     if (n == 0) {  // mod.rs:922-924
         gt_one(out);
@@ -578,7 +623,7 @@ int bn_pairing_batch(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt*
 }
 
 int bn_miller_loop_batch(bn_ctx* c, const bn_g2* q, const bn_g1* p, size_t n, bn_gt* out) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     if (!out || (n && (!p || !q))) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     if (n == 0) {  // the shared loop starts from Fq12::one() (mod.rs:610)
         gt_one(out);
@@ -588,7 +633,7 @@ int bn_miller_loop_batch(bn_ctx* c, const bn_g2* q, const bn_g1* p, size_t n, bn
 }
 
 int bn_final_exponentiation_many(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8_t* ok) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     if (n == 0) return BN_OK;
     if (!f || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     RET_IF(clear_err(c, c->stream));
@@ -597,7 +642,7 @@ int bn_final_exponentiation_many(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out
 }
 
 int bn_miller_loop_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     if (n == 0) return BN_OK;
     if (!p || !q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     for (size_t off = 0; off < n; off += kChunk) {
@@ -638,7 +683,7 @@ int bn_g1_mul_many(bn_ctx* c, const bn_g1* p, const bn_fr* k, size_t n, bn_g1* o
 int bn_g2_mul_many(bn_ctx* c, const bn_g2* p, const bn_fr* k, size_t n, bn_g2* out) { return host_mul(c, p, k, n, out, k_g2_mul); }
 
 int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n, bn_gt* out) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     if (n == 0) return BN_OK;
     if (op < 0 || op > BN_FQ12_FROB3) return fail(c, BN_ERR_INVALID_ARGUMENT, "bad op");
     if (!a || !out || (op == BN_FQ12_MUL && !b)) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
@@ -682,56 +727,56 @@ int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n,
 
 // ---------------------------------------------------------------- encodings / validation
 int bn_fq_from_slice_many(bn_ctx* c, const uint8_t* be32, size_t n, bn_fq* out, uint8_t* st) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{be32, 32}}, {{out, sizeof(bn_fq)}, {st, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_fq_from_slice, (const uint8_t*)d[0], m, (bn_fq*)d[1], (uint8_t*)d[2]);
         return BN_OK;
     });
 }
 int bn_fq_to_big_endian_many(bn_ctx* c, const bn_fq* a, size_t n, uint8_t* be32) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{a, sizeof(bn_fq)}}, {{be32, 32}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_fq_to_be, (const bn_fq*)d[0], m, (uint8_t*)d[1]);
         return BN_OK;
     });
 }
 int bn_fq2_from_slice_many(bn_ctx* c, const uint8_t* be64, size_t n, bn_fq2* out, uint8_t* st) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{be64, 64}}, {{out, sizeof(bn_fq2)}, {st, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_fq2_from_slice, (const uint8_t*)d[0], m, (bn_fq2*)d[1], (uint8_t*)d[2]);
         return BN_OK;
     });
 }
 int bn_fr_from_slice_many(bn_ctx* c, const uint8_t* be32, size_t n, bn_fr* out) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{be32, 32}}, {{out, sizeof(bn_fr)}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_fr_from_slice, (const uint8_t*)d[0], m, (bn_fr*)d[1]);
         return BN_OK;
     });
 }
 int bn_fr_to_big_endian_many(bn_ctx* c, const bn_fr* a, size_t n, uint8_t* be32) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{a, sizeof(bn_fr)}}, {{be32, 32}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_fr_to_be, (const bn_fr*)d[0], m, (uint8_t*)d[1]);
         return BN_OK;
     });
 }
 int bn_fq_sqrt_many(bn_ctx* c, const bn_fq* a, size_t n, bn_fq* out, uint8_t* ok) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{a, sizeof(bn_fq)}}, {{out, sizeof(bn_fq)}, {ok, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_fq_sqrt, (const bn_fq*)d[0], m, (bn_fq*)d[1], (uint8_t*)d[2]);
         return BN_OK;
     });
 }
 int bn_fq2_sqrt_many(bn_ctx* c, const bn_fq2* a, size_t n, bn_fq2* out, uint8_t* ok) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{a, sizeof(bn_fq2)}}, {{out, sizeof(bn_fq2)}, {ok, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_fq2_sqrt, (const bn_fq2*)d[0], m, (bn_fq2*)d[1], (uint8_t*)d[2]);
         return BN_OK;
     });
 }
 int bn_g1_affine_new_many(bn_ctx* c, const bn_fq* x, const bn_fq* y, size_t n, bn_g1* out, uint8_t* st) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{x, sizeof(bn_fq)}, {y, sizeof(bn_fq)}}, {{out, sizeof(bn_g1)}, {st, 1}},
                   [&](void** d, size_t m, hipStream_t s) -> int {
                       KL(k_g1_affine_new, (const bn_fq*)d[0], (const bn_fq*)d[1], m, (bn_g1*)d[2], (uint8_t*)d[3]);
@@ -739,7 +784,7 @@ int bn_g1_affine_new_many(bn_ctx* c, const bn_fq* x, const bn_fq* y, size_t n, b
                   });
 }
 int bn_g2_affine_new_many(bn_ctx* c, const bn_fq2* x, const bn_fq2* y, size_t n, bn_g2* out, uint8_t* st) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{x, sizeof(bn_fq2)}, {y, sizeof(bn_fq2)}}, {{out, sizeof(bn_g2)}, {st, 1}},
                   [&](void** d, size_t m, hipStream_t s) -> int {
                       KL(k_g2_affine_new, (const bn_fq2*)d[0], (const bn_fq2*)d[1], m, (bn_g2*)d[2], (uint8_t*)d[3]);
@@ -756,14 +801,14 @@ int bn_g2_affine_new_many_dev(bn_ctx* c, const bn_fq2* d_x, const bn_fq2* d_y, s
     return BN_OK;
 }
 int bn_g1_from_compressed_many(bn_ctx* c, const uint8_t* b33, size_t n, bn_g1* out, uint8_t* st) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{b33, 33}}, {{out, sizeof(bn_g1)}, {st, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_g1_from_compressed, (const uint8_t*)d[0], m, (bn_g1*)d[1], (uint8_t*)d[2]);
         return BN_OK;
     });
 }
 int bn_g2_from_compressed_many(bn_ctx* c, const uint8_t* b65, size_t n, bn_g2* out, uint8_t* st) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{b65, 65}}, {{out, sizeof(bn_g2)}, {st, 1}}, [&](void** d, size_t m, hipStream_t s) -> int {
         KL(k_g2_from_compressed, (const uint8_t*)d[0], m, (bn_g2*)d[1], (uint8_t*)d[2]);
         return BN_OK;
@@ -795,6 +840,8 @@ int bn_gt_pow_many_dev(bn_ctx* c, const bn_gt* d_a, const bn_fr* d_k, size_t n, 
     if (!d_a || !d_k || !d_out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     RET_IF(reserve(c, n < kChunk ? n : kChunk));
     hipStream_t s = pick(c, stream);
+    RET_IF(ws_acquire(c, s));
+    WsUse use{c, s};
     for (size_t off = 0; off < n; off += kChunk) {
         const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
         KL(k_gt_pow, d_a + off, d_k + off, m, d_out + off, c->slots);
@@ -803,7 +850,7 @@ int bn_gt_pow_many_dev(bn_ctx* c, const bn_gt* d_a, const bn_fr* d_k, size_t n, 
     return BN_OK;
 }
 int bn_gt_pow_many(bn_ctx* c, const bn_gt* a, const bn_fr* k, size_t n, bn_gt* out) {
-    CTX_GUARD(c);
+    CTX_GUARD_HOST(c);
     return staged(c, n, {{a, sizeof(bn_gt)}, {k, sizeof(bn_fr)}}, {{out, sizeof(bn_gt)}},
                   [&](void** d, size_t m, hipStream_t s) -> int {
                       RET_IF(reserve(c, m));

@@ -89,8 +89,12 @@ class Fr:
         return cls(_limbs((v % R_ORDER) * _RM % R_ORDER))
 
     @classmethod
-    def from_str(cls, s):  # fp.rs:23-43 (decimal, reduced mod r)
-        return cls.from_int(int(s, 10)) if s.isdigit() else None
+    def from_str(cls, s):
+        """fp.rs:23-43: ASCII decimal digits only (char::to_digit(10)), reduced mod r;
+        the empty string is zero; any other character gives None."""
+        if not all(c in "0123456789" for c in s):
+            return None
+        return cls.from_int(int(s, 10) if s else 0)
 
     @classmethod
     def one(cls):

@@ -115,6 +115,16 @@ def _arr(a, width):
     return a.reshape(-1, width)
 
 
+def _same_rows(*arrays):
+    """Row count shared by paired inputs; a mismatch raises before any native call
+    (the C ABI reads n rows from every buffer)."""
+    n = arrays[0].shape[0]
+    for a in arrays[1:]:
+        if a.shape[0] != n:
+            raise ValueError("paired inputs have %d and %d rows" % (n, a.shape[0]))
+    return n
+
+
 class Context:
     """One device context (bn_ctx).  All arrays are reference memory images."""
 
@@ -153,26 +163,28 @@ class Context:
     # ---- pairing path
     def pairing_many(self, p, q):
         p, q = _arr(p, 12), _arr(q, 24)
-        if p.shape[0] != q.shape[0]:
-            raise ValueError("p and q lengths differ")
+        _same_rows(p, q)
         out = np.zeros((p.shape[0], 48), np.uint64)
         self._check(self._L.bn_pairing_many(self._h, _ptr(p), _ptr(q), p.shape[0], _ptr(out)))
         return out
 
     def pairing_batch(self, p, q):
         p, q = _arr(p, 12), _arr(q, 24)
+        _same_rows(p, q)
         out = np.zeros(48, np.uint64)
         self._check(self._L.bn_pairing_batch(self._h, _ptr(p), _ptr(q), p.shape[0], _ptr(out)))
         return out
 
     def miller_loop_batch(self, q, p):
         q, p = _arr(q, 24), _arr(p, 12)
+        _same_rows(q, p)
         out = np.zeros(48, np.uint64)
         self._check(self._L.bn_miller_loop_batch(self._h, _ptr(q), _ptr(p), q.shape[0], _ptr(out)))
         return out
 
     def miller_loop_many(self, p, q):
         p, q = _arr(p, 12), _arr(q, 24)
+        _same_rows(p, q)
         out = np.zeros((p.shape[0], 48), np.uint64)
         self._check(self._L.bn_miller_loop_many(self._h, _ptr(p), _ptr(q), p.shape[0], _ptr(out)))
         return out
@@ -187,12 +199,14 @@ class Context:
     # ---- group path
     def g1_mul_many(self, p, k):
         p, k = _arr(p, 12), _arr(k, 4)
+        _same_rows(p, k)
         out = np.zeros_like(p)
         self._check(self._L.bn_g1_mul_many(self._h, _ptr(p), _ptr(k), p.shape[0], _ptr(out)))
         return out
 
     def g2_mul_many(self, p, k):
         p, k = _arr(p, 24), _arr(k, 4)
+        _same_rows(p, k)
         out = np.zeros_like(p)
         self._check(self._L.bn_g2_mul_many(self._h, _ptr(p), _ptr(k), p.shape[0], _ptr(out)))
         return out
@@ -200,6 +214,10 @@ class Context:
     def fq12_op_many(self, op, a, b=None):
         a = _arr(a, 48)
         bb = _arr(b, 48) if b is not None else None
+        if op == "mul":
+            if bb is None:
+                raise ValueError("fq12 mul needs two operands")
+            _same_rows(a, bb)
         out = np.zeros_like(a)
         self._check(self._L.bn_fq12_op_many(self._h, FQ12_OPS[op], _ptr(a), _ptr(bb) if bb is not None else None,
                                             a.shape[0], _ptr(out)))
@@ -280,6 +298,7 @@ class Context:
 
     def g1_affine_new_many(self, x, y):
         x, y = _arr(x, 4), _arr(y, 4)
+        _same_rows(x, y)
         out = np.zeros((x.shape[0], 12), np.uint64)
         st = np.zeros(x.shape[0], np.uint8)
         self._check(self._L.bn_g1_affine_new_many(self._h, _ptr(x), _ptr(y), x.shape[0], _ptr(out), _ptr(st)))
@@ -287,6 +306,7 @@ class Context:
 
     def g2_affine_new_many(self, x, y):
         x, y = _arr(x, 8), _arr(y, 8)
+        _same_rows(x, y)
         out = np.zeros((x.shape[0], 24), np.uint64)
         st = np.zeros(x.shape[0], np.uint8)
         self._check(self._L.bn_g2_affine_new_many(self._h, _ptr(x), _ptr(y), x.shape[0], _ptr(out), _ptr(st)))
@@ -308,6 +328,7 @@ class Context:
 
     def gt_pow_many(self, a, k):
         a, k = _arr(a, 48), _arr(k, 4)
+        _same_rows(a, k)
         out = np.zeros_like(a)
         self._check(self._L.bn_gt_pow_many(self._h, _ptr(a), _ptr(k), a.shape[0], _ptr(out)))
         return out

@@ -98,3 +98,63 @@ def compress_g2(aff):
         rec[i, 0] = 11 if larger else 10
         rec[i, 1:] = np.frombuffer((x1 * P + x0).to_bytes(64, "big"), np.uint8)
     return rec
+
+
+# ---------------------------------------------------------------- the bench dataset
+# bench.py's pairs are indexed globally, so any rank (and any world size) can
+# build exactly the rows it owns: block b (kBlockRows rows) draws its G1 and G2
+# scalars from SplitMix64 seeds DATASET_SEED + 2b and DATASET_SEED + 2b + 1.
+# The scalars are drawn directly as Montgomery Fr images uniform in [1, r)
+# (the image of a uniform scalar is uniform), fully vectorized.
+DATASET_SEED = 1_000_000
+BLOCK_ROWS = 4096
+_GAMMA = np.uint64(0x9E3779B97F4A7C15)
+_R_LIMBS = [(R_ORDER >> (64 * i)) & _M64 for i in range(4)]
+
+
+def _splitmix_draws(seed, first, count):
+    """draws first+1 .. first+count of SplitMix64(seed) (the same stream as SplitMix64.next)."""
+    k = np.arange(first + 1, first + count + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed & _M64) + k * _GAMMA
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def fr_images_raw(n, seed, lo=1):
+    """n Montgomery Fr images uniform in [lo, r), vectorized: candidate j takes draws
+    4j+1..4j+4 as little-endian limbs masked to r's 254 bits and is kept when < r
+    (SplitMix64.below's rule) and >= lo."""
+    top_mask = np.uint64((1 << (R_ORDER.bit_length() - 192)) - 1)
+    out, have, first = [], 0, 0
+    while have < n:
+        m = int((n - have) * 1.4) + 64
+        d = _splitmix_draws(seed, first, 4 * m).reshape(m, 4)
+        first += 4 * m
+        d[:, 3] &= top_mask
+        lt = np.zeros(m, bool)
+        eq = np.ones(m, bool)
+        for i in (3, 2, 1, 0):  # lexicographic compare with r from the top limb
+            li = np.uint64(_R_LIMBS[i])
+            lt |= eq & (d[:, i] < li)
+            eq &= d[:, i] == li
+        ok = lt
+        if lo:
+            nz = (d[:, 0] >= np.uint64(lo)) | (d[:, 1] != 0) | (d[:, 2] != 0) | (d[:, 3] != 0)
+            ok &= nz
+        sel = d[ok]
+        out.append(sel[:n - have])
+        have += min(len(sel), n - have)
+    return np.ascontiguousarray(np.concatenate(out)[:n])
+
+
+def dataset_scalars(lo, n):
+    """(s, t) scalar images of global rows [lo, lo + n) of the bench dataset."""
+    s, t = [], []
+    b0, b1 = lo // BLOCK_ROWS, (lo + n + BLOCK_ROWS - 1) // BLOCK_ROWS
+    for b in range(b0, b1):
+        s.append(fr_images_raw(BLOCK_ROWS, DATASET_SEED + 2 * b))
+        t.append(fr_images_raw(BLOCK_ROWS, DATASET_SEED + 2 * b + 1))
+    off = lo - b0 * BLOCK_ROWS
+    return np.concatenate(s)[off:off + n], np.concatenate(t)[off:off + n]

@@ -1,0 +1,39 @@
+"""bench.py's multi-GPU control flow on CPU (--dry-run-cpu: gloo + a stub engine
+that computes no pairing): `--gpus N` without a launcher starts N ranks itself,
+shards config 4's rows contiguously, all-gathers every chunk inside the step,
+takes the max time over ranks and cross-checks a sample of the next rank's
+rows.  The GPU path of the same code runs in the driver's N-GPU bench."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(args, env=None):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=240, env=e, cwd=ROOT)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_spawns_ranks_config4(world):
+    r = run(["--gpus", str(world), "--dry-run-cpu", "--steps", "1", "--warmup", "1", "--total", "16384",
+             "--chunk", "2048"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == world and line["dry_run"] is True
+    assert line["config"]["workload"].startswith("BASELINE config 4")
+    assert line["config"]["total_pairs"] == 16384 and line["config"]["pairs_per_gpu"] == 16384 // world
+    assert line["scaling"] == "strong" and line["config"]["allgather_in_step"]
+    assert line["cross_rank_check"]["mismatches"] == 0 and line["cross_rank_check"]["ranks_ok"] == world
+
+
+def test_bench_world_size_must_match_gpus():
+    r = run(["--gpus", "2", "--dry-run-cpu"], env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
