@@ -48,12 +48,39 @@ typedef enum {
 
 typedef struct bn_ctx bn_ctx;
 
-/* one context per device; calls on one context are serialized internally */
+/* One context per device.  A context may be shared by host threads: each call holds
+ * it for its whole duration (staging, kernels, readback).  *_dev calls enqueued on
+ * different streams run on the device in call order (the context's workspace is
+ * shared; each call's stream waits for the previous call's work).  The reference
+ * is reentrant from any thread (lib.rs:303-305, Group: Send + Sync). */
 int bn_ctx_create(int device, bn_ctx** out);
 int bn_ctx_destroy(bn_ctx* ctx);
 const char* bn_last_error(const bn_ctx* ctx);
 /* the stream *_dev calls use when given NULL */
 void* bn_ctx_stream(bn_ctx* ctx);
+
+/* ---- several devices of the node in one process ----
+ * A multi-device context shards the host-buffer calls bn_pairing_many,
+ * bn_final_exponentiation_many, bn_miller_loop_many, bn_g1_mul_many and
+ * bn_g2_mul_many contiguously (device k takes bn_shard_range(n, D, k)), runs the
+ * shards concurrently and writes each into the caller's output: the same bytes
+ * as one device.  bn_pairing_batch / bn_miller_loop_batch reduce each shard to
+ * one Miller value, multiply the partials on the first device in device order
+ * (pairing_batch then runs one final exponentiation): the reference's shared
+ * loop value exactly (mod.rs:609-640).  Other calls need a single-device
+ * context: bn_ctx_device(ctx, k) returns device k's (owned by ctx). */
+int bn_ctx_create_multi(const int* devices, int ndev, bn_ctx** out);
+int bn_ctx_num_devices(const bn_ctx* ctx);
+bn_ctx* bn_ctx_device(bn_ctx* ctx, int k);
+/* [*lo, *hi) = shard k of n elements over ndev devices: [k*n/ndev, (k+1)*n/ndev) */
+void bn_shard_range(size_t n, int ndev, int k, size_t* lo, size_t* hi);
+/* BASELINE config 4 in one process: device k computes out = pairing(d_p[k][i], d_q[k][i])
+ * for its n_per_dev HBM-resident pairs, then one RCCL all-gather over xGMI leaves
+ * every d_out[k] (ndev * n_per_dev Gt on device k) holding all results in device
+ * order.  streams[k] (or NULL / a NULL array: the device context's stream) orders
+ * the work on device k.  RCCL (librccl.so.1) is loaded on first use. */
+int bn_pairing_many_allgather_dev(bn_ctx* ctx, const bn_g1* const* d_p, const bn_g2* const* d_q, size_t n_per_dev,
+                                  bn_gt* const* d_out, void* const* streams);
 
 /* ---- pairing path (src/groups/mod.rs:894-926, src/lib.rs:611-633) ---- */
 

@@ -14,38 +14,7 @@
 
 using namespace bn;
 
-// ================================================================ host side
-struct bn_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::mutex mu;
-    std::string err;
-    // workspace (device)
-    size_t cap = 0;  // pairings
-    uint32_t* coeffs = nullptr;
-    uint32_t* paff = nullptr;
-    uint32_t* slots = nullptr;  // Fq12 slots of the step machine; slot 0 = Miller values
-    uint8_t* flags = nullptr;
-    uint32_t* d_prog = nullptr; // final-exponentiation step program
-    // optional per-phase timing of bn_pairing_many_dev (HIP events on the launch stream)
-    bool timing = false;
-    std::vector<hipEvent_t> ev_pool;
-    std::vector<std::array<hipEvent_t, 5>> ev_marks;
-    int fe_steps = 0;
-    int fe_out = 0;
-    int* d_err = nullptr;
-    // staging for host-buffer calls (device)
-    size_t stage_bytes = 0;
-    void* stage = nullptr;
-    // The workspace (coeffs, paff, slots, flags, d_err, stage) is shared by every
-    // call on this context.  Host-side, the mutex serializes the calls; device-side,
-    // every workspace user records ws_event on its stream when it has enqueued its
-    // work, and the next user's stream waits on that event first (WsUse), so _dev
-    // calls on different caller streams run in call order instead of racing on the
-    // same buffers.  No caller stream is remembered past its call.
-    hipEvent_t ws_event = nullptr;
-    bool ws_pending = false;
-};
+#include "ctx.h"
 
 namespace {
 
@@ -301,6 +270,9 @@ int clear_err(bn_ctx* c, hipStream_t s) {
 
 #define CTX_GUARD(ctx)                                 \
     if (!(ctx)) return BN_ERR_INVALID_ARGUMENT;        \
+    if (!(ctx)->subs.empty())                          \
+        return fail((ctx), BN_ERR_INVALID_ARGUMENT,    \
+                    "not available on a multi-device context; use bn_ctx_device()"); \
     std::lock_guard<std::mutex> lock_((ctx)->mu);      \
     HIPCHK(ctx, hipSetDevice((ctx)->device))
 #define RET_IF(x)              \
@@ -408,6 +380,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
 
 int bn_ctx_destroy(bn_ctx* c) {
     if (!c) return BN_ERR_INVALID_ARGUMENT;
+    if (!c->subs.empty()) return bn_multi_destroy(c);
     (void)hipSetDevice(c->device);
     if (c->ws_pending) (void)hipEventSynchronize(c->ws_event);
     (void)hipStreamSynchronize(c->stream);
@@ -429,6 +402,10 @@ void* bn_ctx_stream(bn_ctx* c) { return c ? (void*)c->stream : nullptr; }
 size_t bn_workspace_bytes(size_t n) { return ws_bytes(n); }
 
 int bn_reserve(bn_ctx* c, size_t n) {
+    if (c && !c->subs.empty()) {
+        for (bn_ctx* d : c->subs) RET_IF(bn_reserve(d, n / c->subs.size() + 1));
+        return BN_OK;
+    }
     CTX_GUARD(c);
     return reserve(c, n < kChunk ? n : kChunk);
 }
@@ -509,6 +486,7 @@ int bn_get_phase_times(bn_ctx* c, float* ms, int* launches) {
 }
 
 int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
+    if (c && !c->subs.empty()) return bn_multi_pairing_many(c, p, q, n, out);
     CTX_GUARD_HOST(c);  // held for the whole call: staging, kernels, readback
     if (n == 0) return BN_OK;
     if (!p || !q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
@@ -574,7 +552,16 @@ static int miller_product(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, i
     return BN_OK;
 }
 
-static void gt_one(bn_gt* out) {  // Fq12::one() image: c0.c0.c0 = R mod p
+// the Miller product of n host pairs on one single-device context (its lock held)
+int bn_internal_miller_product(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, int mode, bn_gt* result) {
+    CTX_GUARD_HOST(c);
+    RET_IF(miller_product(c, p, q, n, mode, result));
+    return BN_OK;
+}
+
+void bn_internal_gt_one(bn_gt* out);
+static void gt_one(bn_gt* out) { bn_internal_gt_one(out); }
+void bn_internal_gt_one(bn_gt* out) {  // Fq12::one() image: c0.c0.c0 = R mod p
     memset(out, 0, sizeof(bn_gt));
     out->c[0].l[0] = 0xd35d438dc58f0d9dull;
     out->c[0].l[1] = 0x0a78eb28f5c70b3dull;
@@ -607,6 +594,7 @@ static int final_exp_host(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8
 }
 
 int bn_pairing_batch(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
+    if (c && !c->subs.empty()) return bn_multi_pairing_batch(c, p, q, n, out);
     CTX_GUARD_HOST(c);
     if (!out || (n && (!p || !q))) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     if (n == 0) {  // mod.rs:922-924
@@ -623,6 +611,7 @@ int bn_pairing_batch(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt*
 }
 
 int bn_miller_loop_batch(bn_ctx* c, const bn_g2* q, const bn_g1* p, size_t n, bn_gt* out) {
+    if (c && !c->subs.empty()) return bn_multi_miller_loop_batch(c, q, p, n, out);
     CTX_GUARD_HOST(c);
     if (!out || (n && (!p || !q))) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
     if (n == 0) {  // the shared loop starts from Fq12::one() (mod.rs:610)
@@ -633,6 +622,7 @@ int bn_miller_loop_batch(bn_ctx* c, const bn_g2* q, const bn_g1* p, size_t n, bn
 }
 
 int bn_final_exponentiation_many(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8_t* ok) {
+    if (c && !c->subs.empty()) return bn_multi_final_exponentiation_many(c, f, n, out, ok);
     CTX_GUARD_HOST(c);
     if (n == 0) return BN_OK;
     if (!f || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
@@ -642,6 +632,7 @@ int bn_final_exponentiation_many(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out
 }
 
 int bn_miller_loop_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
+    if (c && !c->subs.empty()) return bn_multi_miller_loop_many(c, p, q, n, out);
     CTX_GUARD_HOST(c);
     if (n == 0) return BN_OK;
     if (!p || !q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
@@ -679,8 +670,14 @@ int bn_g2_mul_many_dev(bn_ctx* c, const bn_g2* d_p, const bn_fr* d_k, size_t n, 
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
-int bn_g1_mul_many(bn_ctx* c, const bn_g1* p, const bn_fr* k, size_t n, bn_g1* out) { return host_mul(c, p, k, n, out, k_g1_mul); }
-int bn_g2_mul_many(bn_ctx* c, const bn_g2* p, const bn_fr* k, size_t n, bn_g2* out) { return host_mul(c, p, k, n, out, k_g2_mul); }
+int bn_g1_mul_many(bn_ctx* c, const bn_g1* p, const bn_fr* k, size_t n, bn_g1* out) {
+    if (c && !c->subs.empty()) return bn_multi_g1_mul_many(c, p, k, n, out);
+    return host_mul(c, p, k, n, out, k_g1_mul);
+}
+int bn_g2_mul_many(bn_ctx* c, const bn_g2* p, const bn_fr* k, size_t n, bn_g2* out) {
+    if (c && !c->subs.empty()) return bn_multi_g2_mul_many(c, p, k, n, out);
+    return host_mul(c, p, k, n, out, k_g2_mul);
+}
 
 int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n, bn_gt* out) {
     CTX_GUARD_HOST(c);

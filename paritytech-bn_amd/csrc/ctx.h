@@ -1,0 +1,64 @@
+// ctx.h -- the bn_ctx behind the C ABI (host side, shared by capi.hip and
+// capi_multi.hip).  Not a public header.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <mutex>
+#include <string>
+#include <vector>
+
+struct bn_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string err;
+    // workspace (device)
+    size_t cap = 0;  // pairings
+    uint32_t* coeffs = nullptr;
+    uint32_t* paff = nullptr;
+    uint32_t* slots = nullptr;  // Fq12 slots of the step machine; slot 0 = Miller values
+    uint8_t* flags = nullptr;
+    uint32_t* d_prog = nullptr; // final-exponentiation step program
+    // optional per-phase timing of bn_pairing_many_dev (HIP events on the launch stream)
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::array<hipEvent_t, 5>> ev_marks;
+    int fe_steps = 0;
+    int fe_out = 0;
+    int* d_err = nullptr;
+    // staging for host-buffer calls (device)
+    size_t stage_bytes = 0;
+    void* stage = nullptr;
+    // The workspace (coeffs, paff, slots, flags, d_err, stage) is shared by every
+    // call on this context.  Host-side, the mutex serializes the calls; device-side,
+    // every workspace user records ws_event on its stream when it has enqueued its
+    // work, and the next user's stream waits on that event first (WsUse), so _dev
+    // calls on different caller streams run in call order instead of racing on the
+    // same buffers.  No caller stream is remembered past its call.
+    hipEvent_t ws_event = nullptr;
+    bool ws_pending = false;
+    // multi-device context (bn_ctx_create_multi): one single-device sub-context
+    // per listed device; `device` is -1 and the fields above are unused
+    std::vector<bn_ctx*> subs;
+    std::vector<int> devices;
+    void* comms = nullptr;  // RCCL communicators (capi_multi.hip), created on first use
+};
+
+
+// capi_multi.hip: the multi-device forms of the host-buffer entry points
+#include "../../include/bn254mi.h"
+#define BN_HIDDEN __attribute__((visibility("hidden")))
+extern "C" {  // internal (not in bn254mi.h); C linkage matches their definitions' scope
+BN_HIDDEN int bn_multi_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out);
+BN_HIDDEN int bn_multi_pairing_batch(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out);
+BN_HIDDEN int bn_multi_miller_loop_batch(bn_ctx* c, const bn_g2* q, const bn_g1* p, size_t n, bn_gt* out);
+BN_HIDDEN int bn_multi_final_exponentiation_many(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8_t* ok);
+BN_HIDDEN int bn_multi_miller_loop_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out);
+BN_HIDDEN int bn_multi_g1_mul_many(bn_ctx* c, const bn_g1* p, const bn_fr* k, size_t n, bn_g1* out);
+BN_HIDDEN int bn_multi_g2_mul_many(bn_ctx* c, const bn_g2* p, const bn_fr* k, size_t n, bn_g2* out);
+BN_HIDDEN int bn_multi_destroy(bn_ctx* c);
+// capi.hip internals used by capi_multi.hip
+BN_HIDDEN int bn_internal_miller_product(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, int mode, bn_gt* result);
+BN_HIDDEN void bn_internal_gt_one(bn_gt* out);
+}

@@ -33,6 +33,7 @@ EXPORTS = [
     "bn_fr_to_big_endian_many", "bn_fq_sqrt_many", "bn_fq2_sqrt_many", "bn_g1_affine_new_many",
     "bn_g2_affine_new_many", "bn_g2_affine_new_many_dev", "bn_g1_from_compressed_many", "bn_g2_from_compressed_many",
     "bn_g1_from_compressed_many_dev", "bn_g2_from_compressed_many_dev", "bn_gt_pow_many", "bn_gt_pow_many_dev",
+    "bn_ctx_create_multi", "bn_ctx_num_devices", "bn_ctx_device", "bn_shard_range", "bn_pairing_many_allgather_dev",
 ]
 
 # per-element status (bn_elem_status)
@@ -95,6 +96,11 @@ def load():
         "bn_g2_from_compressed_many_dev": ([vp, vp, sz, vp, vp, vp], i),
         "bn_gt_pow_many": ([vp, vp, vp, sz, vp], i),
         "bn_gt_pow_many_dev": ([vp, vp, vp, sz, vp, vp], i),
+        "bn_ctx_create_multi": ([vp, i, ctypes.POINTER(vp)], i),
+        "bn_ctx_num_devices": ([vp], i),
+        "bn_ctx_device": ([vp, i], vp),
+        "bn_shard_range": ([sz, i, i, ctypes.POINTER(sz), ctypes.POINTER(sz)], None),
+        "bn_pairing_many_allgather_dev": ([vp, vp, vp, sz, vp, vp], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -125,17 +131,42 @@ def _same_rows(*arrays):
     return n
 
 
-class Context:
-    """One device context (bn_ctx).  All arrays are reference memory images."""
+def shard_range(n, ndev, k):
+    """[lo, hi) of shard k of n elements over ndev devices (the C ABI's split)."""
+    lo, hi = ctypes.c_size_t(), ctypes.c_size_t()
+    load().bn_shard_range(n, ndev, k, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
 
-    def __init__(self, device=0):
+
+class Context:
+    """One device context (bn_ctx), or with `devices=[...]` one context over several
+    devices of the node (bn_ctx_create_multi).  All arrays are reference memory images."""
+
+    def __init__(self, device=0, devices=None):
         L = load()
         h = ctypes.c_void_p()
-        rc = L.bn_ctx_create(device, ctypes.byref(h))
+        if devices is None:
+            rc = L.bn_ctx_create(device, ctypes.byref(h))
+        else:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = L.bn_ctx_create_multi(arr, len(devices), ctypes.byref(h))
         if rc != BN_OK:
-            raise BnError(rc, "bn_ctx_create(device=%d) failed" % device)
+            raise BnError(rc, "bn_ctx_create(%s) failed" % (device if devices is None else devices))
         self._h = h
         self._L = L
+
+    @property
+    def num_devices(self):
+        return self._L.bn_ctx_num_devices(self._h)
+
+    def pairing_many_allgather_dev(self, d_p, d_q, n_per_dev, d_out, streams=None):
+        """Config 4 in one process: per-device pointer lists (ints); every d_out[k]
+        receives all num_devices * n_per_dev results in device order."""
+        nd = len(d_p)
+        vp = ctypes.c_void_p
+        arr = lambda xs: (vp * nd)(*xs)  # noqa: E731
+        self._check(self._L.bn_pairing_many_allgather_dev(self._h, arr(d_p), arr(d_q), n_per_dev, arr(d_out),
+                                                          arr(streams) if streams else None))
 
     def close(self):
         if getattr(self, "_h", None):

@@ -55,3 +55,18 @@ def test_workspace_size_is_sane(lib):
     lib.bn_workspace_bytes.argtypes = [ctypes.c_size_t]
     per = lib.bn_workspace_bytes(1 << 16) / (1 << 16)
     assert 15_000 < per < 40_000   # ~19 KB of line coefficients + Fq12 slots per pairing
+
+
+def test_shard_range_is_contiguous_and_covers(lib):
+    """bn_shard_range (the multi-device split) -- host arithmetic, no GPU."""
+    from substrate_bn import _native, parallel
+    for n in (0, 1, 7, 65536, (1 << 20) + 3):
+        for nd in (1, 2, 3, 8):
+            lo_prev = 0
+            for k in range(nd):
+                lo, hi = _native.shard_range(n, nd, k)
+                assert lo == lo_prev and hi >= lo
+                assert (lo, hi) == tuple(parallel.shard_bounds(n, k, nd))
+                lo_prev = hi
+            assert lo_prev == n
+    assert _native.shard_range(10, 2, 2) == (0, 0)  # k out of range

@@ -1,0 +1,64 @@
+"""Multi-device context of the C ABI (bn_ctx_create_multi) on the
+one-GPU box: a context over devices [0, 0] runs two sub-contexts on the same
+MI355X, which exercises the contiguous sharding, the concurrent per-device
+threads and the partial-product combination exactly as on 8 devices; the RCCL
+all-gather form runs as a world of one (ncclCommInitAll over [0]).  Results
+must equal the single-device engine and the oracle bit for bit."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+NT = 16
+
+
+@pytest.fixture(scope="module")
+def data():
+    p, q, _, _ = O.random_pairs(101, seed=909, nthreads=NT)
+    z = p.copy()
+    z[5] = 0
+    z[5, 4:8] = O.canon_to_mont_array([1])  # a zero point: one for pairing, skipped by pairing_batch
+    return {"p": p, "q": q, "pz": z, "gt": O.pairing_many(z, q, NT), "prod": O.pairing_batch(z, q)}
+
+
+@pytest.fixture(scope="module")
+def mctx():
+    from substrate_bn import Context
+    return Context(devices=[0, 0])
+
+
+def test_multi_context_shards_host_calls(mctx, data):
+    assert mctx.num_devices == 2
+    assert np.array_equal(mctx.pairing_many(data["pz"], data["q"]), data["gt"])
+    assert np.array_equal(mctx.pairing_batch(data["pz"], data["q"]), data["prod"])
+    ks, K = O.random_scalars(101, seed=910, lo=0)
+    assert np.array_equal(mctx.g1_mul_many(data["p"], K), O.g1_mul(data["p"], K, NT))
+    ml = mctx.miller_loop_many(data["p"][:9], data["q"][:9])
+    out, ok = mctx.final_exponentiation_many(ml)
+    assert ok.all() and np.array_equal(out, O.pairing_many(data["p"][:9], data["q"][:9], NT))
+    # miller_loop_batch: product of the per-device partials equals the oracle's shared loop
+    _, want = O.miller_loop_batch(data["q"][:33], data["p"][:33])
+    assert np.array_equal(mctx.miller_loop_batch(data["q"][:33], data["p"][:33]), want)
+    # fewer elements than devices: an empty shard
+    assert np.array_equal(mctx.pairing_many(data["p"][:1], data["q"][:1]), O.pairing_many(data["p"][:1], data["q"][:1]))
+
+
+def test_multi_context_refuses_single_device_calls(mctx, data):
+    from substrate_bn import BnError
+    with pytest.raises(BnError):
+        mctx.gt_pow_many(data["gt"][:2], np.zeros((2, 4), np.uint64))
+
+
+def test_allgather_dev_world_of_one(data):
+    import torch
+    from substrate_bn import Context
+    ctx = Context(devices=[0])
+    dev = torch.device("cuda", 0)
+    P = torch.from_numpy(data["pz"].view(np.int64)).to(dev)
+    Q = torch.from_numpy(data["q"].view(np.int64)).to(dev)
+    out = torch.zeros((101, 48), dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream(dev)
+    ctx.pairing_many_allgather_dev([P.data_ptr()], [Q.data_ptr()], 101, [out.data_ptr()], [s.cuda_stream])
+    torch.cuda.synchronize(dev)
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), data["gt"])
