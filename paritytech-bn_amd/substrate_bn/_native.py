@@ -58,6 +58,14 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise ImportError("libbn254mi.so not built: run `make -C paritytech-bn_amd` "
                           "(or __graft_entry__.build())")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (and HSA
+    # runtime).  Loaded first, it satisfies this library's libamdhip64.so.7 by
+    # SONAME, so engine calls and torch tensors/streams/RCCL share one runtime;
+    # loaded the other way round the process would hold two runtimes.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, sz, i, u8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p
     sig = {
