@@ -52,7 +52,7 @@ int ws_drain(bn_ctx* c) {
 constexpr int kFeSlots = 32;  // slot 0: Miller value, 1: easy-part result, 2..: temporaries
 
 size_t ws_bytes(size_t n) {
-    return n * ((size_t)kCoeffFq * 9 * 4 + 2 * 9 * 4 + (size_t)kFeSlots * kSlotWords * 4 + 1) + 64;
+    return n * ((size_t)kCoeffFq * 9 * 4 + kPathLanes * (2 * 9 * 4 + 1) + (size_t)kFeSlots * kSlotWords * 4) + 64;
 }
 
 // ---------------------------------------------------------------- FE step program
@@ -205,9 +205,9 @@ int reserve(bn_ctx* c, size_t n) {
     if (c->flags) HIPCHK(c, hipFree(c->flags));
     c->coeffs = nullptr; c->paff = nullptr; c->slots = nullptr; c->flags = nullptr; c->cap = 0;
     HIPCHK(c, hipMalloc(&c->coeffs, n * (size_t)kCoeffFq * 9 * 4));
-    HIPCHK(c, hipMalloc(&c->paff, n * 2 * 9 * 4));
+    HIPCHK(c, hipMalloc(&c->paff, n * kPathLanes * 2 * 9 * 4));
     HIPCHK(c, hipMalloc(&c->slots, n * (size_t)kFeSlots * kSlotWords * 4));
-    HIPCHK(c, hipMalloc(&c->flags, n));
+    HIPCHK(c, hipMalloc(&c->flags, n * kPathLanes));
     c->cap = n;
     return BN_OK;
 }
@@ -228,9 +228,9 @@ hipStream_t pick(bn_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
 // Miller values of n pairs into slot 0 (lane-strided, stride = n); n <= c->cap
 int miller_values(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int mode, hipStream_t s) {
-    k_prepare<<<grid_for(n), kBlock, 0, s>>>(d_p, d_q, n, c->coeffs, c->paff, c->flags, c->d_err, mode);
+    k_prepare<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(d_p, d_q, n, c->coeffs, c->paff, c->flags, c->d_err, mode);
     HIPCHK(c, hipGetLastError());
-    k_miller<<<grid_for(n), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, n, c->slots);
+    k_miller<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, n, c->slots);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
@@ -238,7 +238,7 @@ int miller_values(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int m
 int product_tree(bn_ctx* c, size_t n, hipStream_t s) {
     for (size_t m = n; m > 1;) {
         const size_t half = (m + 1) / 2;
-        k_fq12_product<<<grid_for(half), kBlock, 0, s>>>(c->slots, n, m, half);
+        k_fq12_product<<<grid_for(kPathLanes * half), kBlock, 0, s>>>(c->slots, n, m, half);
         HIPCHK(c, hipGetLastError());
         m = half;
     }
@@ -247,9 +247,9 @@ int product_tree(bn_ctx* c, size_t n, hipStream_t s) {
 
 // final exponentiation of the n values in slot 0 -> out (device Gt images)
 int run_fe(bn_ctx* c, size_t n, const uint8_t* flags, bn_gt* out, uint8_t* ok, hipStream_t s) {
-    k_fq12_vm<<<grid_for(n), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, n);
+    k_fq12_vm<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, n);
     HIPCHK(c, hipGetLastError());
-    k_fe_out<<<grid_for(n), kBlock, 0, s>>>(c->slots, n, c->fe_out, flags, out, ok, c->d_err);
+    k_fe_out<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(c->slots, n, c->fe_out, flags, out, ok, c->d_err);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
@@ -438,13 +438,13 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             if (c->timing && ev[k]) hipEventRecord(ev[k], s);
         };
         mark(0);
-        k_prepare<<<grid_for(m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags, c->d_err, 0);
+        k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags, c->d_err, 0);
         mark(1);
-        k_miller<<<grid_for(m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, c->slots);
+        k_miller<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, c->slots);
         mark(2);
-        k_fq12_vm<<<grid_for(m), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, m);
+        k_fq12_vm<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, m);
         mark(3);
-        k_fe_out<<<grid_for(m), kBlock, 0, s>>>(c->slots, m, c->fe_out, c->flags, d_out + off, nullptr, c->d_err);
+        k_fe_out<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->slots, m, c->fe_out, c->flags, d_out + off, nullptr, c->d_err);
         mark(4);
         HIPCHK(c, hipGetLastError());
         if (c->timing) c->ev_marks.push_back(ev);
@@ -543,7 +543,7 @@ static int miller_product(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, i
     bn_gt* d = (bn_gt*)c->stage;
     HIPCHK(c, hipMemcpyAsync(d, parts.data(), np * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
     RET_IF(reserve(c, np));
-    k_gt_load<<<grid_for(np), kBlock, 0, c->stream>>>(d, np, c->slots);
+    k_gt_load<<<grid_for(kPathLanes * np), kBlock, 0, c->stream>>>(d, np, c->slots);
     RET_IF(product_tree(c, np, c->stream));
     k_gt_store<<<1, kBlock, 0, c->stream>>>(c->slots, 1, np, d + np);
     HIPCHK(c, hipGetLastError());
@@ -580,7 +580,7 @@ static int final_exp_host(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8
         bn_gt* dout = din + m;
         uint8_t* dok = (uint8_t*)(dout + m);
         HIPCHK(c, hipMemcpyAsync(din, f + off, m * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
-        k_gt_load<<<grid_for(m), kBlock, 0, c->stream>>>(din, m, c->slots);
+        k_gt_load<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(din, m, c->slots);
         HIPCHK(c, hipGetLastError());
         RET_IF(run_fe(c, m, nullptr, dout, dok, c->stream));
         HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
@@ -646,7 +646,7 @@ int bn_miller_loop_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_
         HIPCHK(c, hipMemcpyAsync(dp, p + off, m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
         RET_IF(miller_values(c, dp, dq, m, 0, c->stream));
-        k_gt_store<<<grid_for(m), kBlock, 0, c->stream>>>(c->slots, m, m, dout);
+        k_gt_store<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(c->slots, m, m, dout);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -693,10 +693,10 @@ int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n,
         bn_gt* dout = db + m;
         uint32_t* dprog = (uint32_t*)(dout + m);
         HIPCHK(c, hipMemcpyAsync(da, a + off, m * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
-        k_gt_load<<<grid_for(m), kBlock, 0, c->stream>>>(da, m, c->slots + (size_t)1 * kSlotWords * m);
+        k_gt_load<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(da, m, c->slots + (size_t)1 * kSlotWords * m);
         if (op == BN_FQ12_MUL) {
             HIPCHK(c, hipMemcpyAsync(db, b + off, m * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
-            k_gt_load<<<grid_for(m), kBlock, 0, c->stream>>>(db, m, c->slots + (size_t)2 * kSlotWords * m);
+            k_gt_load<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(db, m, c->slots + (size_t)2 * kSlotWords * m);
         }
         Prog P;
         P.next = 3;
@@ -713,8 +713,8 @@ int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n,
         }
         P.finalize({res});
         HIPCHK(c, hipMemcpyAsync(dprog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice, c->stream));
-        k_fq12_vm<<<grid_for(m), kBlock, 0, c->stream>>>(dprog, P.steps(), c->slots, m);
-        k_gt_store<<<grid_for(m), kBlock, 0, c->stream>>>(c->slots + (size_t)res * kSlotWords * m, m, m, dout);
+        k_fq12_vm<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(dprog, P.steps(), c->slots, m);
+        k_gt_store<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(c->slots + (size_t)res * kSlotWords * m, m, m, dout);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));

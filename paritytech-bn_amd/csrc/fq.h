@@ -40,6 +40,13 @@
 #ifndef BN_FENCE_FQ
 #define BN_FENCE_FQ 0
 #endif
+// Layout of the pairing-path kernels: 1 = two lanes per element (fq2_split.h),
+// 0 = one lane per element.  A pairing-path translation unit sets
+// BN_SPLIT = BN_PATH_SPLIT before including kernels.h; every other unit
+// (host side, group and codec kernels) keeps BN_SPLIT = 0.
+#ifndef BN_PATH_SPLIT
+#define BN_PATH_SPLIT 1
+#endif
 
 namespace bn {
 

@@ -1,0 +1,259 @@
+// fq2_split.h -- Fq2 = Fq[u]/(u^2+1) with TWO lanes per element (BN_SPLIT;
+// included by tower.h inside namespace bn).
+//
+// Lanes 2j and 2j+1 of a wave hold coordinate c0 and c1 of element j.  Every
+// Fq2 operation below computes this lane's coordinate of the result; the
+// other coordinate, when needed, comes from the partner lane over DPP
+// (quad_perm [1,0,3,2]: one v_mov_b32_dpp per 32-bit digit).  Additions,
+// subtractions, halving, folds and scaling by an Fq are lane-local: each lane
+// does half of the unsplit work.  A product is one column sum of two digit
+// products per lane, reduced once -- lane 0: a0*b0 + a1*(K*p - b1), lane 1:
+// a0*b1 + a1*b0 -- i.e. exactly one coordinate of fq2_mul_sb.
+//
+// Why: with one lane per element a batch of 2^16 pairings is 1024 waves, one
+// per SIMD, and a lone wave issues one VALU instruction every ~6 cycles
+// whatever the instruction; two waves per SIMD issue the digit-wise VOP2 work
+// 2.5x faster and MADs ~15 % faster (profiles/r2d_valu_ubench.jsonl).  Split
+// lanes give 2048 waves for the same batch, and each lane holds half the
+// state (an Fq12 is 54 VGPRs), so two waves fit the register file.
+//
+// Bit-exactness: each lane computes the same residue as the corresponding
+// coordinate of the one-lane formulas (the same ring identities), and values
+// are canonicalized only at the boundary.
+
+template <int B>
+struct Fq2 {
+    Fq<B> c;  // this lane's coordinate: c0 on even lanes, c1 on odd lanes
+};
+
+BN_INLINE bool lane_odd() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (__builtin_amdgcn_workitem_id_x() & 1u) != 0;
+#else
+    return false;
+#endif
+}
+// the partner lane's copy of a 32-bit value (lanes 2j <-> 2j+1)
+BN_INLINE uint32_t swap_pair(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+#else
+    return v;
+#endif
+}
+template <int B>
+BN_INLINE Fq<B> fq_partner(const Fq<B>& a) {
+    Fq<B> r;
+#pragma unroll
+    for (int l = 0; l < 9; ++l) r.v[l] = swap_pair(a.v[l]);
+    return r;
+}
+template <int K>
+BN_INLINE Fq2<K> wrap2(const Fq<K>& x) { return {x}; }
+
+template <int B2, int B>
+BN_INLINE Fq2<B2> widen(const Fq2<B>& a) { return {widen<B2>(a.c)}; }
+
+BN_INLINE Fq2<1> fq2_const(const Limbs9& c0, const Limbs9& c1) {
+    return {fq_select(lane_odd(), fq_from_limbs<1>(c1), fq_from_limbs<1>(c0))};
+}
+BN_INLINE Fq2<1> fq2_zero() { return {fq_zero()}; }
+BN_INLINE Fq2<1> fq2_one() { return {fq_select(lane_odd(), fq_zero(), fq_one())}; }
+template <int B>
+BN_INLINE Fq2<B> fq2_select(bool c, const Fq2<B>& a, const Fq2<B>& b) { return {fq_select(c, a.c, b.c)}; }
+template <int A, int B>
+BN_INLINE auto fq2_add(const Fq2<A>& a, const Fq2<B>& b) { return wrap2(fq_add(a.c, b.c)); }
+template <int A, int B>
+BN_INLINE auto fq2_sub(const Fq2<A>& a, const Fq2<B>& b) { return wrap2(fq_sub(a.c, b.c)); }
+template <int B>
+BN_INLINE auto fq2_neg(const Fq2<B>& a) { return wrap2(fq_neg(a.c)); }
+template <int B>
+BN_INLINE auto fq2_dbl(const Fq2<B>& a) { return fq2_add(a, a); }
+template <int B>
+BN_INLINE Fq2<2> fq2_fold(const Fq2<B>& a) { return {fq_fold(a.c)}; }
+template <int B>
+BN_INLINE Fq2<kv(B)> fq2_norm(const Fq2<B>& a) { return {fq_norm(a.c)}; }
+template <int B>
+BN_INLINE auto fq2_half(const Fq2<B>& a) { return wrap2(fq_half(a.c)); }
+// fq2.rs:48-53 (s must hold the same value on both lanes of the element)
+template <int A, int B>
+BN_INLINE auto fq2_scale(const Fq2<A>& a, const Fq<B>& s) { return wrap2(fq_mul(a.c, s)); }
+template <int L, int B>
+BN_INLINE auto pre(const Fq2<B>& a) {
+    if constexpr (kv(B) <= L) return a; else return fq2_fold(a);
+}
+// both lanes agree: element zero iff both coordinates are
+template <int B>
+BN_INLINE bool fq2_is_zero(const Fq2<B>& a) {
+    const uint32_t z = fq_is_zero(a.c) ? 1u : 0u;
+    return (z & swap_pair(z)) != 0;
+}
+template <int A, int B>
+BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) {
+    const uint32_t e = fq_eq(a.c, b.c) ? 1u : 0u;
+    return (e & swap_pair(e)) != 0;
+}
+#ifndef BN_FQ2_FENCE
+#define BN_FQ2_FENCE 1
+#endif
+template <int B>
+BN_INLINE void fq2_fence(Fq2<B>& a) {
+#if BN_FQ2_FENCE
+    fq_fence(a.c);
+#else
+    (void)a;
+#endif
+}
+
+// K*p - x without a carry pass (digits < (L+2)*2^29, value <= (B+1)*p)
+template <int K>
+BN_INLINE Fq<kenc(kv(K) + 1, kl(K) + 2)> fq_neg_lazy(const Fq<K>& x) {
+    constexpr Limbs9 Q = kp_spread(kv(K) + 1, kl(K));
+    Fq<kenc(kv(K) + 1, kl(K) + 2)> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = Q.v[i] - x.v[i];
+    return r;
+}
+// per-lane choice between two values of different static types (the join)
+template <int A, int B>
+BN_INLINE Fq<kjoin(A, B)> fq_pick(bool c, const Fq<A>& a, const Fq<B>& b) {
+    Fq<kjoin(A, B)> r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+    return r;
+}
+
+// REDC(x*y + z*w): one Montgomery reduction of a two-product column sum (the
+// fq_mul column scan with a second product per column).  Column sums stay
+// below 2^64 when Lx*Ly + Lz*Lw <= 6.
+template <int X, int Y, int Z, int W>
+BN_INLINE auto fq_dot2(const Fq<X>& x, const Fq<Y>& y, const Fq<Z>& z, const Fq<W>& w) {
+    static_assert(kl(X) * kl(Y) + kl(Z) * kl(W) <= 6, "fq_dot2: column sum could overflow 64 bits");
+    constexpr int BO = 1 + (int)(((long long)kv(X) * kv(Y) + (long long)kv(Z) * kv(W)) * 5908 / 1000000 + 1);
+    uint32_t m[9];
+    Fq<BO> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        const int lo = k < 9 ? 0 : k - 8;
+        const int hi = k < 9 ? k : 8;
+#pragma unroll
+        for (int i = lo; i <= hi; ++i) {
+            acc += (uint64_t)x.v[i] * y.v[k - i];
+            acc += (uint64_t)z.v[i] * w.v[k - i];
+        }
+#pragma unroll
+        for (int i = lo; i <= hi; ++i)
+            if (i < k) acc += (uint64_t)m[i] * kP29.v[k - i];
+        if (k < 9) {
+            m[k] = ((uint32_t)acc * BN_PINV29) & M29;
+            acc += (uint64_t)m[k] * kP29.v[0];
+        } else {
+            r.v[k - 9] = (uint32_t)acc & M29;
+        }
+        acc >>= 29;
+    }
+    r.v[8] = (uint32_t)acc;
+    return r;
+}
+
+// fq2.rs:136-148 (the same residues as fq2_mul_sb): lane 0 computes
+// c0 = a0*b0 + a1*(K*p - b1), lane 1 computes c1 = a1*b0 + a0*b1, both as
+// own_a * Y + partner_a * W with per-lane operand choice.
+template <int A, int B>
+BN_INLINE auto fq2_mul_split(const Fq2<A>& a, const Fq2<B>& b) {
+    if constexpr (kl(A) * (2 * kl(B) + 2) > 6) {
+        if constexpr (kl(B) * (2 * kl(A) + 2) <= 6) return fq2_mul_split(b, a);
+        else if constexpr (kl(A) >= kl(B)) return fq2_mul_split(fq2_norm(a), b);
+        else return fq2_mul_split(a, fq2_norm(b));
+    } else {
+        const bool odd = lane_odd();
+        const Fq<A> pa = fq_partner(a.c);
+        const Fq<B> pb = fq_partner(b.c);
+        const Fq<B> y = fq_select(odd, pb, b.c);
+        const auto w = fq_pick(odd, b.c, fq_neg_lazy(pb));
+        return wrap2(fq_dot2(a.c, y, pa, w));
+    }
+}
+template <int A, int B>
+BN_INLINE auto fq2_mul(const Fq2<A>& a_in, const Fq2<B>& b_in) {
+    if constexpr (kv(A) > 40 || kv(B) > 40) return fq2_mul(pre<40>(a_in), pre<40>(b_in)); else {
+    Fq2<A> a = a_in;
+    Fq2<B> b = b_in;
+    fq2_fence(a);
+    fq2_fence(b);
+    auto r = fq2_mul_split(a, b);
+    fq2_fence(r);
+    return r;
+    }
+}
+template <class R, class S>
+struct Fq2Pair {
+    R a;
+    S b;
+};
+template <int A, int B, int C, int D>
+BN_INLINE auto fq2_mul2(const Fq2<A>& a_in, const Fq2<B>& b_in, const Fq2<C>& c_in, const Fq2<D>& d_in) {
+    if constexpr (kv(A) > 40 || kv(B) > 40 || kv(C) > 40 || kv(D) > 40) {
+        return fq2_mul2(pre<40>(a_in), pre<40>(b_in), pre<40>(c_in), pre<40>(d_in));
+    } else {
+        Fq2<A> a = a_in;
+        Fq2<B> b = b_in;
+        Fq2<C> c = c_in;
+        Fq2<D> d = d_in;
+        fq2_fence(a);
+        fq2_fence(b);
+        fq2_fence(c);
+        fq2_fence(d);
+        auto r = fq2_mul_split(a, b);
+        auto q = fq2_mul_split(c, d);
+        fq2_fence(r);
+        fq2_fence(q);
+        return Fq2Pair<decltype(r), decltype(q)>{r, q};
+    }
+}
+
+// fq2.rs:105-117: c0 = (a0 - a1)(a0 + a1), c1 = 2*a0*a1 -- one product per lane:
+// lane 0: (a0 + K*p - a1) * (a0 + a1), lane 1: a1 * (2*a0)
+template <int A>
+BN_INLINE auto fq2_sqr(const Fq2<A>& a_in) {
+    if constexpr (kv(A) > 40) return fq2_sqr(fq2_fold(a_in)); else {
+    Fq2<A> a = a_in;
+    fq2_fence(a);
+    const bool odd = lane_odd();
+    const Fq<kv(A)> own = fq_norm(a.c);
+    const Fq<kv(A)> par = fq_partner(own);
+    const auto x = fq_norm(fq_pick(odd, own, fq_sub(own, par)));
+    const auto y = fq_pick(odd, fq_add(par, par), fq_add(own, par));
+    auto r = wrap2(fq_mul(x, y));
+    fq2_fence(r);
+    return r;
+    }
+}
+// x * xi, xi = 9 + u (fq2.rs:19-34, 55-57): lane 0: 9a0 - a1, lane 1: 9a1 + a0.
+template <int A>
+BN_INLINE auto fq2_mul_xi(const Fq2<A>& a) {
+    if constexpr (kv(A) > 8) {
+        return fq2_mul_xi(fq2_fold(a));
+    } else {
+        const Fq<kv(A)> own = fq_norm(a.c);
+        const auto own9 = fq_add(fq_mul_small<8>(own), own);
+        const Fq<kv(A)> par = fq_partner(own);
+        return wrap2(fq_add(own9, fq_pick(lane_odd(), par, fq_neg_lazy(par))));
+    }
+}
+// fq2.rs:59-68: odd powers conjugate: lane 1 negates (c1 * (p-1) == -c1)
+template <int B>
+BN_INLINE auto fq2_conj(const Fq2<B>& a) {
+    const Fq<kv(B)> own = fq_norm(a.c);
+    return wrap2(fq_select(lane_odd(), fq_neg(own), own));
+}
+// fq2.rs:119-130: t = (c0^2 + c1^2)^-1 on both lanes, then (c0 t, -c1 t)
+template <int B>
+BN_INLINE auto fq2_inv(const Fq2<B>& a_in) {
+    auto a = pre<40>(a_in);
+    const auto sq = fq_sqr(a.c);
+    const auto t = fq_inv(fq_add(sq, fq_partner(sq)));  // the same norm on both lanes
+    const auto r = fq_mul(a.c, t);
+    return wrap2(fq_select(lane_odd(), fq_neg(r), r));
+}

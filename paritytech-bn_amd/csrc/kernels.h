@@ -12,6 +12,19 @@ namespace bn {
 // per SIMD (measured census, profiles/r1_ubench3.jsonl); 64-thread workgroups
 // left 104 of 1024 SIMDs with two waves while others idled.
 constexpr int kBlock = 256;
+// The pairing-path kernels (kernels_pairing/fe/util.hip) run two lanes per
+// element (fq2_split.h: 2^16 pairings -> 2048 waves, two per SIMD); the host
+// launches kPathLanes threads per element.  Built with -DBN_PATH_SPLIT=0 they
+// run the one-lane layout (the round-1 form, kept for A/B measurements).
+constexpr int kPathLanes = BN_PATH_SPLIT ? 2 : 1;
+// words of one Fq12 slot per lane of the translation unit's own layout
+constexpr int kSlotLaneWords = BN_SPLIT ? 54 : 108;
+#if BN_SPLIT
+// two waves per SIMD: the kernel must fit 256 registers
+#define BN_PATH_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+#else
+#define BN_PATH_ATTR
+#endif
 constexpr int kCoeffFq = BN_NUM_COEFFS * 6;  // Fq elements of line coefficients per pairing
 constexpr size_t kChunk = size_t(1) << 18;   // pairings per launch set (~5 GB workspace)
 constexpr int kSlotWords = 108;              // one Fq12: 12 Fq x 9 digits
@@ -29,6 +42,19 @@ __device__ __forceinline__ Fq<B> ld_fq(const uint32_t* base, size_t n, size_t i,
     for (int l = 0; l < 9; ++l) x.v[l] = base[((size_t)j * 9 + l) * n + i];
     return x;
 }
+#if BN_SPLIT
+// Two lanes per element (fq2_split.h): `n` counts LANES and `i` is the lane;
+// an Fq2 "slot" j (even, as in the one-lane layout) holds the lane's own
+// coordinate at word ((j/2)*9 + l)*n + i, so a wave touches 256 contiguous bytes.
+template <int B>
+__device__ __forceinline__ void st_fq2(uint32_t* base, size_t n, size_t i, int j, const Fq2<B>& x) {
+    st_fq(base, n, i, j / 2, x.c);
+}
+template <int B>
+__device__ __forceinline__ Fq2<B> ld_fq2(const uint32_t* base, size_t n, size_t i, int j) {
+    return {ld_fq<B>(base, n, i, j / 2)};
+}
+#else
 template <int B>
 __device__ __forceinline__ void st_fq2(uint32_t* base, size_t n, size_t i, int j, const Fq2<B>& x) {
     st_fq(base, n, i, j, x.c0);
@@ -38,6 +64,7 @@ template <int B>
 __device__ __forceinline__ Fq2<B> ld_fq2(const uint32_t* base, size_t n, size_t i, int j) {
     return {ld_fq<B>(base, n, i, j), ld_fq<B>(base, n, i, j + 1)};
 }
+#endif
 template <int B>
 __device__ __forceinline__ void st_fq12(uint32_t* base, size_t n, size_t i, const Fq12<B>& f) {
     st_fq2(base, n, i, 0, f.c0.c0);
@@ -72,6 +99,23 @@ __device__ __forceinline__ void st_fq_buf(__amdgpu_buffer_rsrc_t rs, int vo, siz
 #pragma unroll
     for (int l = 0; l < 9; ++l) __builtin_amdgcn_raw_buffer_store_b32(x.v[l], rs, vo, (int)(((size_t)j * 9 + l) * n * 4), 0);
 }
+#if BN_SPLIT
+template <int B>
+__device__ __forceinline__ void st_fq12_buf(uint32_t* base, size_t n, size_t i, const Fq12<B>& f) {
+    const auto rs = slot_rsrc(base);
+    const int vo = (int)(i * 4);
+    const Fq2<B>* c[6] = {&f.c0.c0, &f.c0.c1, &f.c0.c2, &f.c1.c0, &f.c1.c1, &f.c1.c2};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) st_fq_buf(rs, vo, n, k, c[k]->c);
+}
+template <int B>
+__device__ __forceinline__ Fq12<B> ld_fq12_buf(const uint32_t* base, size_t n, size_t i) {
+    const auto rs = slot_rsrc(base);
+    const int vo = (int)(i * 4);
+    auto q = [&](int k) { return Fq2<B>{ld_fq_buf<B>(rs, vo, n, k)}; };
+    return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
+}
+#else
 template <int B>
 __device__ __forceinline__ void st_fq12_buf(uint32_t* base, size_t n, size_t i, const Fq12<B>& f) {
     const auto rs = slot_rsrc(base);
@@ -91,6 +135,8 @@ __device__ __forceinline__ Fq12<B> ld_fq12_buf(const uint32_t* base, size_t n, s
     return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
 }
 
+#endif  // BN_SPLIT
+
 // Per-lane slot selection (Gt::pow's window table): the descriptor is built
 // from the uniform workspace base and the lane's slot goes into the VGPR
 // offset, so the resource stays wave-uniform.  A descriptor built from a
@@ -99,6 +145,7 @@ __device__ __forceinline__ Fq12<B> ld_fq12_buf(const uint32_t* base, size_t n, s
 // regions; round 1's k_gt_pow faulted with an illegal address in that form
 // (DESIGN.md §3).  vo_bytes = (slot * kSlotWords * n + i) * 4 must stay below
 // 2^31 (checked by the host launcher).
+#if !BN_SPLIT
 template <int B>
 __device__ __forceinline__ Fq12<B> ld_fq12_buf_sel(const uint32_t* ws, size_t n, uint32_t vo_bytes) {
     const auto rs = slot_rsrc(ws);
@@ -106,6 +153,7 @@ __device__ __forceinline__ Fq12<B> ld_fq12_buf_sel(const uint32_t* ws, size_t n,
     auto q = [&](int k) { return Fq2<B>{ld_fq_buf<B>(rs, vo, n, 2 * k), ld_fq_buf<B>(rs, vo, n, 2 * k + 1)}; };
     return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
 }
+#endif
 
 template <int B>
 __device__ __forceinline__ Fq6<B> ld_fq6(const uint32_t* base, size_t n, size_t i, int h) {
@@ -140,6 +188,7 @@ __device__ __forceinline__ auto fq6_mul_g(const Fq6<A>& a, G&& g) {
     }
 }
 
+#if !BN_SPLIT
 // a * b (fq12.rs:319-327 Karatsuba) with b read per Fq2 from `y`, the calling
 // lane's strided copy of an Fq12 (word w at y[w * stride]: an LDS image with
 // stride kBlock, or a lane-strided HBM slot with stride n); conj_b multiplies
@@ -170,6 +219,8 @@ __device__ __forceinline__ Fq12<kF> mul12_strided(const Fq12<kF>& a, const uint3
 __device__ __forceinline__ Fq12<kF> mul12_lds(const Fq12<kF>& a, const uint32_t* yl, bool conj_b) {
     return mul12_strided(a, yl, kBlock, conj_b);
 }
+
+#endif
 
 // Asynchronous copy of a lane-strided Fq12 (108 words, stride n) from global
 // memory into the block's LDS image (stride kBlock) with buffer_load ... lds:
@@ -215,12 +266,47 @@ __device__ __forceinline__ void st_ref(bn_fq& a, const Fq<B>& x) {
     fq_store_ref(x, w);
     st_words(&a, w);
 }
+#if BN_SPLIT
+// this lane's coordinate of a reference Fq2 image (c0 on even lanes, c1 on odd)
+__device__ __forceinline__ Fq2<2> ld_ref2(const bn_fq2& a) { return {ld_ref(lane_odd() ? a.c1 : a.c0)}; }
+template <int B>
+__device__ __forceinline__ void st_ref2(bn_fq2& a, const Fq2<B>& x) {
+    st_ref(lane_odd() ? a.c1 : a.c0, x.c);
+}
+#else
 __device__ __forceinline__ Fq2<2> ld_ref2(const bn_fq2& a) { return {ld_ref(a.c0), ld_ref(a.c1)}; }
 template <int B>
 __device__ __forceinline__ void st_ref2(bn_fq2& a, const Fq2<B>& x) {
     st_ref(a.c0, x.c0);
     st_ref(a.c1, x.c1);
 }
+#endif
+#if BN_SPLIT
+// Gt image: coefficient 2k + (lane parity) is the lane's coordinate of Fq2 k in
+// the order c0.c0, c0.c1, c0.c2, c1.c0, c1.c1, c1.c2 (fq12.rs:52-55)
+template <int B>
+__device__ __forceinline__ void st_gt(bn_gt& g, const Fq12<B>& f) {
+    const int o = lane_odd() ? 1 : 0;
+    st_ref(g.c[0 + o], f.c0.c0.c);
+    st_ref(g.c[2 + o], f.c0.c1.c);
+    st_ref(g.c[4 + o], f.c0.c2.c);
+    st_ref(g.c[6 + o], f.c1.c0.c);
+    st_ref(g.c[8 + o], f.c1.c1.c);
+    st_ref(g.c[10 + o], f.c1.c2.c);
+}
+__device__ __forceinline__ Fq12<2> ld_gt(const bn_gt& g) {
+    const int o = lane_odd() ? 1 : 0;
+    auto q = [&](int k) { return Fq2<2>{ld_ref(g.c[2 * k + o])}; };
+    return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
+}
+// the lane's half of the zero image
+__device__ __forceinline__ void st_gt_zero(bn_gt& g) {
+    uint32_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int o = lane_odd() ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) st_words(&g.c[2 * k + o], z);
+}
+#else
 template <int B>
 __device__ __forceinline__ void st_gt(bn_gt& g, const Fq12<B>& f) {
     // coefficient order c0.c0.c0, c0.c0.c1, c0.c1.c0, ... (fq12.rs:52-55); no array
@@ -247,6 +333,7 @@ __device__ __forceinline__ void st_gt_zero(bn_gt& g) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) st_words(&g.c[k], z);
 }
+#endif  // BN_SPLIT
 
 // Fr Montgomery image -> canonical scalar words: U256::from(Fr), fp.rs:13-20
 // (one REDC by r with 32-bit digits; once per scalar product)

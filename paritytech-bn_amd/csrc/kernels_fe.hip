@@ -1,34 +1,40 @@
 // kernels_fe.hip -- final exponentiation (fq12.rs:62-124, 249-266) as a step
 // program over lane-strided Fq12 slots (see kernels.h), plus the Gt output.
+// Pairing-path layout (BN_PATH_SPLIT: two lanes per element, fq2_split.h);
+// `n` counts elements, the grid has kPathLanes threads per element.
 // fq_fold reads -q*p from an LDS table (fq.h; every kernel here calls
 // fold_table_init first): 2-3 % faster on this path, measured
 #ifndef BN_FOLD_LDS
 #define BN_FOLD_LDS 1
 #endif
+#include "fq.h"
+#define BN_SPLIT BN_PATH_SPLIT
 #include "kernels.h"
 
 namespace bn {
 
-__device__ __forceinline__ uint32_t* slot_ptr(uint32_t* slots, size_t n, uint32_t s) {
-    return slots + (size_t)s * kSlotWords * n;
+constexpr size_t kL = BN_SPLIT ? 2 : 1;  // lanes per element in this translation unit
+
+__device__ __forceinline__ uint32_t* slot_ptr(uint32_t* slots, size_t nl, uint32_t s) {
+    return slots + (size_t)s * kSlotLaneWords * nl;
 }
 
-__global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps, uint32_t* slots,
-                                                    size_t n) {
+__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps,
+                                                                uint32_t* slots, size_t n) {
     fold_table_init();
     const size_t i = lane_id();
-    if (i >= n) return;
+    if (i >= kL * n) return;
     Fq12<kF> acc = widen<kF>(fq12_one());  // the previous step's result, kept in registers
 #pragma unroll 1
     for (int pc = 0; pc < nsteps; ++pc) {
         const uint32_t ins = prog[2 * pc];  // uniform: scalar loads
         const uint32_t aux = prog[2 * pc + 1];
         const uint32_t op = ins & 0xff, k = aux & 0xff, flags = aux >> 8;
-        // The slot stride passes through an empty asm once per step, so the 108
-        // word offsets of a lane-strided Fq12 (w * n, uniform) are rebuilt where
+        // The slot stride passes through an empty asm once per step, so the
+        // word offsets of a lane-strided Fq12 (w * nl, uniform) are rebuilt where
         // they are used instead of being hoisted out of the step loop, where they
         // would occupy ~216 SGPRs and spill through VGPR lanes.
-        size_t nn = n;
+        size_t nn = kL * n;
         asm volatile("" : "+s"(nn));
         uint32_t* d = slot_ptr(slots, nn, (ins >> 8) & 0xff);
         const uint32_t* a = slot_ptr(slots, nn, (ins >> 16) & 0xff);
@@ -65,25 +71,29 @@ __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__
     }
 }
 
-// out[i] = slot `out_slot`; slot 0 holds the Miller value: f == 0 means the
+// out[e] = slot `out_slot`; slot 0 holds the Miller value: f == 0 means the
 // reference returns None (fq12.rs:63-72) and pairing() panics -> zero Gt,
-// ok[i] = 0, error bit.  flags[i] (a zero input point) -> Fq12::one().
-__global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot,
-                                                   const uint8_t* __restrict__ flags, bn_gt* __restrict__ out,
-                                                   uint8_t* __restrict__ ok, int* __restrict__ err) {
+// ok[e] = 0, error bit.  flags[lane] (a zero input point) -> Fq12::one().
+// Both lanes of an element hold the same flag and reach the same zero test
+// (fq2_is_zero combines the two coordinates), so control flow is per element.
+__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot,
+                                                               const uint8_t* __restrict__ flags, bn_gt* __restrict__ out,
+                                                               uint8_t* __restrict__ ok, int* __restrict__ err) {
     fold_table_init();
-    const size_t i = lane_id();
-    if (i >= n) return;
+    const size_t i = lane_id(), e = i / kL;
+    if (e >= n) return;
+    const size_t nl = kL * n;
+    const bool lead = (i % kL) == 0;
     const bool skip = flags && flags[i];
-    const bool zero = !skip && fq12_is_zero(ld_fq12<kF>(slots, n, i));
-    if (ok) ok[i] = zero ? 0 : 1;
+    const bool zero = !skip && fq12_is_zero(ld_fq12<kF>(slots, nl, i));
+    if (ok && lead) ok[e] = zero ? 0 : 1;
     if (zero) {
-        if (err) atomicOr(err, 1 << BN_ERR_FE_ZERO);
-        st_gt_zero(out[i]);
+        if (err && lead) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        st_gt_zero(out[e]);
     } else if (skip) {
-        st_gt(out[i], fq12_one());
+        st_gt(out[e], fq12_one());
     } else {
-        st_gt(out[i], ld_fq12<kF>(slots + (size_t)out_slot * kSlotWords * n, n, i));
+        st_gt(out[e], ld_fq12<kF>(slots + (size_t)out_slot * kSlotLaneWords * nl, nl, i));
     }
 }
 

@@ -29,17 +29,120 @@ namespace bn {
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
+// ---------------------------------------------------------------- inversion
+// Fermat: a^(p-2).  Inverses are unique, so this equals the reference's binary
+// extended Euclid (arith.rs:324-370 + fp.rs:108-117) bit for bit, without its
+// data-dependent control flow.  The chain is the windowed plan below (fq_inv_w).
+// ---------------------------------------------------------------- fixed-exponent windowed powers
+// Left-to-right sliding window of width 4 for a constant exponent, planned at
+// compile time as (squarings, odd digit) steps.  The exponent is the same in
+// every lane, so the digit dispatch is a scalar branch.  x^e is unique, so any
+// chain gives the reference's value (fields/mod.rs:35-46 square-and-multiply).
+struct PowPlan {
+    int first = 0, n = 0;
+    uint8_t sq[96] = {};
+    uint8_t dig[96] = {};
+};
+constexpr bool pbit(const uint64_t (&e)[4], int i) { return (e[i >> 6] >> (i & 63)) & 1u; }
+constexpr PowPlan pow_plan(const uint64_t (&e)[4], int top) {
+    PowPlan c;
+    int i = top, pend = 0;
+    bool first = true;
+    while (i >= 0) {
+        if (!pbit(e, i)) {
+            ++pend;
+            --i;
+            continue;
+        }
+        int j = i - 3 < 0 ? 0 : i - 3;
+        while (!pbit(e, j)) ++j;
+        int v = 0;
+        for (int k = i; k >= j; --k) v = 2 * v + (pbit(e, k) ? 1 : 0);
+        if (first) {
+            c.first = v;
+            first = false;
+        } else {
+            c.sq[c.n] = (uint8_t)(pend + i - j + 1);
+            c.dig[c.n] = (uint8_t)v;
+            ++c.n;
+        }
+        pend = 0;
+        i = j - 1;
+    }
+    if (pend) {
+        c.sq[c.n] = (uint8_t)pend;
+        c.dig[c.n] = 0;
+        ++c.n;
+    }
+    return c;
+}
+constexpr uint64_t kPm2[4] = {0x3c208c16d87cfd45ull, 0x97816a916871ca8dull, 0xb85045b68181585dull,
+                              0x30644e72e131a029ull};  // p - 2
+constexpr PowPlan kInvPlan = pow_plan(kPm2, 253);
+
+template <int B>
+BN_INLINE Fq<2> fq_pow_plan(const Fq<B>& a, const PowPlan& c) {
+    const Fq<2> x1 = widen<2>(fq_reduce(a));
+    const Fq<2> x2 = fq_sqr(x1);
+    const Fq<2> x3 = fq_mul(x1, x2), x5 = fq_mul(x3, x2), x7 = fq_mul(x5, x2), x9 = fq_mul(x7, x2);
+    const Fq<2> x11 = fq_mul(x9, x2), x13 = fq_mul(x11, x2), x15 = fq_mul(x13, x2);
+    auto times = [&](const Fq<2>& r, int d) -> Fq<2> {
+        switch (d) {
+            case 1: return fq_mul(r, x1);
+            case 3: return fq_mul(r, x3);
+            case 5: return fq_mul(r, x5);
+            case 7: return fq_mul(r, x7);
+            case 9: return fq_mul(r, x9);
+            case 11: return fq_mul(r, x11);
+            case 13: return fq_mul(r, x13);
+            case 15: return fq_mul(r, x15);
+            default: return r;
+        }
+    };
+    Fq<2> r;
+    switch (c.first) {
+        case 1: r = x1; break;
+        case 3: r = x3; break;
+        case 5: r = x5; break;
+        case 7: r = x7; break;
+        case 9: r = x9; break;
+        case 11: r = x11; break;
+        case 13: r = x13; break;
+        default: r = x15; break;
+    }
+#pragma unroll 1
+    for (int s = 0; s < c.n; ++s) {
+        const int q = c.sq[s];
+#pragma unroll 1
+        for (int k = 0; k < q; ++k) r = fq_sqr(r);
+        r = times(r, c.dig[s]);
+    }
+    return r;
+}
+// Fermat inversion a^(p-2) by the windowed plan (253 squarings, ~55 products
+// instead of the binary chain's ~126): the same unique inverse
+template <int B>
+BN_INLINE Fq<2> fq_inv_w(const Fq<B>& a) { return fq_pow_plan(a, kInvPlan); }
+template <int B>
+BN_INLINE Fq<2> fq_inv(const Fq<B>& a) { return fq_inv_w(a); }
+// x unchanged when its bound is <= L, else folded to 2 (decided at compile time)
+template <int L, int B>
+BN_INLINE auto pre(const Fq<B>& a) {
+    if constexpr (kv(B) <= L) return a; else return fq_fold(a);
+}
+
+// Fq2: one lane per element (below), or with BN_SPLIT two lanes per element,
+// one coordinate each (fq2_split.h)
+#ifndef BN_SPLIT
+#define BN_SPLIT 0
+#endif
+#if BN_SPLIT
+#include "fq2_split.h"
+#else
+
 template <int B>
 struct Fq2 {
     Fq<B> c0, c1;
-};
-template <int B>
-struct Fq6 {
-    Fq2<B> c0, c1, c2;
-};
-template <int B>
-struct Fq12 {
-    Fq6<B> c0, c1;
 };
 
 // ================================================================ Fq2 = Fq[u]/(u^2+1)
@@ -78,11 +181,6 @@ template <int B>
 BN_INLINE bool fq2_is_zero(const Fq2<B>& a) {
     const bool z0 = fq_is_zero(a.c0), z1 = fq_is_zero(a.c1);
     return z0 && z1;
-}
-// x unchanged when its bound is <= L, else folded to 2 (decided at compile time)
-template <int L, int B>
-BN_INLINE auto pre(const Fq<B>& a) {
-    if constexpr (kv(B) <= L) return a; else return fq_fold(a);
 }
 template <int L, int B>
 BN_INLINE auto pre(const Fq2<B>& a) {
@@ -325,103 +423,6 @@ BN_INLINE auto fq2_mul_xi(const Fq2<A>& a) {
 template <int B>
 BN_INLINE auto fq2_conj(const Fq2<B>& a) { return mk2(a.c0, fq_neg(a.c1)); }
 
-// ---------------------------------------------------------------- inversion
-// Fermat: a^(p-2).  Inverses are unique, so this equals the reference's binary
-// extended Euclid (arith.rs:324-370 + fp.rs:108-117) bit for bit, without its
-// data-dependent control flow.  The chain is the windowed plan below (fq_inv_w).
-// ---------------------------------------------------------------- fixed-exponent windowed powers
-// Left-to-right sliding window of width 4 for a constant exponent, planned at
-// compile time as (squarings, odd digit) steps.  The exponent is the same in
-// every lane, so the digit dispatch is a scalar branch.  x^e is unique, so any
-// chain gives the reference's value (fields/mod.rs:35-46 square-and-multiply).
-struct PowPlan {
-    int first = 0, n = 0;
-    uint8_t sq[96] = {};
-    uint8_t dig[96] = {};
-};
-constexpr bool pbit(const uint64_t (&e)[4], int i) { return (e[i >> 6] >> (i & 63)) & 1u; }
-constexpr PowPlan pow_plan(const uint64_t (&e)[4], int top) {
-    PowPlan c;
-    int i = top, pend = 0;
-    bool first = true;
-    while (i >= 0) {
-        if (!pbit(e, i)) {
-            ++pend;
-            --i;
-            continue;
-        }
-        int j = i - 3 < 0 ? 0 : i - 3;
-        while (!pbit(e, j)) ++j;
-        int v = 0;
-        for (int k = i; k >= j; --k) v = 2 * v + (pbit(e, k) ? 1 : 0);
-        if (first) {
-            c.first = v;
-            first = false;
-        } else {
-            c.sq[c.n] = (uint8_t)(pend + i - j + 1);
-            c.dig[c.n] = (uint8_t)v;
-            ++c.n;
-        }
-        pend = 0;
-        i = j - 1;
-    }
-    if (pend) {
-        c.sq[c.n] = (uint8_t)pend;
-        c.dig[c.n] = 0;
-        ++c.n;
-    }
-    return c;
-}
-constexpr uint64_t kPm2[4] = {0x3c208c16d87cfd45ull, 0x97816a916871ca8dull, 0xb85045b68181585dull,
-                              0x30644e72e131a029ull};  // p - 2
-constexpr PowPlan kInvPlan = pow_plan(kPm2, 253);
-
-template <int B>
-BN_INLINE Fq<2> fq_pow_plan(const Fq<B>& a, const PowPlan& c) {
-    const Fq<2> x1 = widen<2>(fq_reduce(a));
-    const Fq<2> x2 = fq_sqr(x1);
-    const Fq<2> x3 = fq_mul(x1, x2), x5 = fq_mul(x3, x2), x7 = fq_mul(x5, x2), x9 = fq_mul(x7, x2);
-    const Fq<2> x11 = fq_mul(x9, x2), x13 = fq_mul(x11, x2), x15 = fq_mul(x13, x2);
-    auto times = [&](const Fq<2>& r, int d) -> Fq<2> {
-        switch (d) {
-            case 1: return fq_mul(r, x1);
-            case 3: return fq_mul(r, x3);
-            case 5: return fq_mul(r, x5);
-            case 7: return fq_mul(r, x7);
-            case 9: return fq_mul(r, x9);
-            case 11: return fq_mul(r, x11);
-            case 13: return fq_mul(r, x13);
-            case 15: return fq_mul(r, x15);
-            default: return r;
-        }
-    };
-    Fq<2> r;
-    switch (c.first) {
-        case 1: r = x1; break;
-        case 3: r = x3; break;
-        case 5: r = x5; break;
-        case 7: r = x7; break;
-        case 9: r = x9; break;
-        case 11: r = x11; break;
-        case 13: r = x13; break;
-        default: r = x15; break;
-    }
-#pragma unroll 1
-    for (int s = 0; s < c.n; ++s) {
-        const int q = c.sq[s];
-#pragma unroll 1
-        for (int k = 0; k < q; ++k) r = fq_sqr(r);
-        r = times(r, c.dig[s]);
-    }
-    return r;
-}
-// Fermat inversion a^(p-2) by the windowed plan (253 squarings, ~55 products
-// instead of the binary chain's ~126): the same unique inverse
-template <int B>
-BN_INLINE Fq<2> fq_inv_w(const Fq<B>& a) { return fq_pow_plan(a, kInvPlan); }
-template <int B>
-BN_INLINE Fq<2> fq_inv(const Fq<B>& a) { return fq_inv_w(a); }
-
 // fq2.rs:119-130
 template <int B>
 BN_INLINE auto fq2_inv(const Fq2<B>& a_in) {
@@ -429,6 +430,19 @@ BN_INLINE auto fq2_inv(const Fq2<B>& a_in) {
     auto t = fq_inv(fq_add(fq_sqr(a.c0), fq_sqr(a.c1)));  // c0^2 - (p-1) c1^2
     return mk2(fq_mul(a.c0, t), fq_neg(fq_mul(a.c1, t)));
 }
+
+BN_INLINE Fq2<1> fq2_const(const Limbs9& c0, const Limbs9& c1) { return {fq_from_limbs<1>(c0), fq_from_limbs<1>(c1)}; }
+
+#endif  // BN_SPLIT
+
+template <int B>
+struct Fq6 {
+    Fq2<B> c0, c1, c2;
+};
+template <int B>
+struct Fq12 {
+    Fq6<B> c0, c1;
+};
 
 // ================================================================ Fq6 = Fq2[v]/(v^3 - xi)
 template <int A, int B, int C>
@@ -452,7 +466,7 @@ template <int B>
 BN_INLINE auto fq6_neg(const Fq6<B>& a) { return mk6(fq2_neg(a.c0), fq2_neg(a.c1), fq2_neg(a.c2)); }
 template <int B>
 BN_INLINE Fq6<2> fq6_fold(const Fq6<B>& a) {
-#if BN_FOLD_LDS && defined(__HIP_DEVICE_COMPILE__)
+#if BN_FOLD_LDS && defined(__HIP_DEVICE_COMPILE__) && !BN_SPLIT
     if constexpr (kl(B) <= 6) {
         const FoldEnt e0 = fold_fetch(a.c0.c0), e1 = fold_fetch(a.c0.c1), e2 = fold_fetch(a.c1.c0),
                       e3 = fold_fetch(a.c1.c1), e4 = fold_fetch(a.c2.c0), e5 = fold_fetch(a.c2.c1);
@@ -525,7 +539,6 @@ BN_INLINE auto fq6_inv(const Fq6<B>& a_in) {
 }
 
 // Frobenius coefficients (internal form, generated from fq6.rs:5-90 / fq12.rs:6-48)
-BN_INLINE Fq2<1> fq2_const(const Limbs9& c0, const Limbs9& c1) { return {fq_from_limbs<1>(c0), fq_from_limbs<1>(c1)}; }
 BN_INLINE Fq2<1> fq6_frob_c1(int n) {
     if (n == 1) return fq2_const(Limbs9{BN_FQ6_C1_1_C0}, Limbs9{BN_FQ6_C1_1_C1});
     if (n == 2) return fq2_const(Limbs9{BN_FQ6_C1_2_C0}, Limbs9{BN_FQ6_C1_2_C1});
@@ -545,7 +558,7 @@ BN_INLINE Fq2<1> fq12_frob_c1(int n) {
 template <int POWER, int B>
 BN_INLINE auto fq6_frobenius_map(const Fq6<B>& a) {
     if constexpr (POWER == 2) {
-        return mk6(a.c0, fq2_scale(a.c1, fq6_frob_c1(2).c0), fq2_scale(a.c2, fq6_frob_c2(2).c0));
+        return mk6(a.c0, fq2_scale(a.c1, fq_from_limbs<1>(Limbs9{BN_FQ6_C1_2_C0})), fq2_scale(a.c2, fq_from_limbs<1>(Limbs9{BN_FQ6_C2_2_C0})));
     } else {
         return mk6(fq2_conj(a.c0), fq2_mul(fq2_conj(a.c1), fq6_frob_c1(POWER)), fq2_mul(fq2_conj(a.c2), fq6_frob_c2(POWER)));
     }
@@ -608,10 +621,11 @@ BN_INLINE auto fq12_inv(const Fq12<B>& a_in) {
 template <int POWER, int B>
 BN_INLINE auto fq12_frobenius_map(const Fq12<B>& a) {
     auto c1 = fq6_frobenius_map<POWER>(a.c1);
-    Fq2<1> k = fq12_frob_c1(POWER);
     if constexpr (POWER == 2) {
-        return mk12(fq6_frobenius_map<POWER>(a.c0), mk6(fq2_scale(c1.c0, k.c0), fq2_scale(c1.c1, k.c0), fq2_scale(c1.c2, k.c0)));
+        const Fq<1> k = fq_from_limbs<1>(Limbs9{BN_FQ12_C1_2_C0});  // real: fq12.rs:6-48 power 2 has c1 == 0
+        return mk12(fq6_frobenius_map<POWER>(a.c0), mk6(fq2_scale(c1.c0, k), fq2_scale(c1.c1, k), fq2_scale(c1.c2, k)));
     } else {
+        Fq2<1> k = fq12_frob_c1(POWER);
         return mk12(fq6_frobenius_map<POWER>(a.c0), mk6(fq2_mul(c1.c0, k), fq2_mul(c1.c1, k), fq2_mul(c1.c2, k)));
     }
 }
