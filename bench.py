@@ -168,7 +168,8 @@ def other_workload(args, local_rank):
 
     dev = torch.device("cuda", local_rank)
     ctx = Context(local_rank)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # a real stream: handle 0 would mean the context's own stream
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
     res = {"n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)", "data": "synthetic"}
@@ -185,22 +186,55 @@ def other_workload(args, local_rank):
         n = args.pairs if args.pairs != (1 << 16) else (1 << 14)
         Pd, Qd = device_points(ctx, n, 21, 22, dev, sh)
         p, q = Pd.cpu().numpy().view(np.uint64), Qd.cpu().numpy().view(np.uint64)
-        step = lambda: ctx.pairing_batch(p, q)  # noqa: E731
+        gout = torch.zeros(48, dtype=torch.int64, device=dev)
+        gst = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        step = lambda: ctx.pairing_batch_dev(Pd.data_ptr(), Qd.data_ptr(), n, gout.data_ptr(),  # noqa: E731
+                                             gst.data_ptr(), sh)
         unit = "pairing-product terms/s"
-        res["config"] = {"workload": "BASELINE config 5: one pairing_batch over 2^14 terms (per-term Miller "
-                                     "values, product tree, one final exponentiation; host buffers incl. PCIe)",
-                         "terms": n}
+        res["config"] = {"workload": "BASELINE config 5: one pairing_batch over 2^14 terms, HBM-resident inputs "
+                                     "(bn_pairing_batch_dev: per-term lines + Miller values, device product "
+                                     "reduction and one final exponentiation on 16-lane groups)", "terms": n}
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record(stream)
     for _ in range(args.steps):
         step()
+    e1.record(stream)
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     res.update({"metric": unit, "value": n * args.steps / el, "unit": unit, "ms_per_step": el / args.steps * 1e3})
     from oracle import oracle as O  # the checker (cpu_baseline leg)
-    if args.workload == "g1mul":
+    if args.workload == "product":
+        # SURVEY 8(d) config 5 algorithmic work: per term to_affine 19 + precompute 2,655 + lines 3,741
+        # Fq-mul; the 64 shared squarings (2,304) and one final exponentiation (8,767) once per product
+        work = (n * (19 + 2655 + 3741) + 2304 + 8767) * MAD32_PER_FQMUL
+        ms = e0.elapsed_time(e1) / args.steps
+        res["roofline"] = {"bound": "valu", "achieved": work / (ms * 1e-3) / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
+                           "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)",
+                           "frac": work / (ms * 1e-3) / PEAK_MAD32_PER_S, "traffic": None,
+                           "kernel": "whole product (k_prepare, k_miller, k_fq12_reduce_wide x2, k_fe_wide)",
+                           "per_step_ms": ms,
+                           "basis": "SURVEY.md 8(d) config 5: n*(19+2655+3741) + 2304 + 8767 Fq-mul, x128 MAD32"}
+        threads = host_cpus()["usable"]
+        t0 = time.perf_counter()
+        ref = O.pairing_batch(p, q, nthreads=threads)
+        dt = time.perf_counter() - t0
+        m1 = min(1024, n)
+        t0 = time.perf_counter()
+        O.pairing_batch(p[:m1], q[:m1])
+        dt1 = time.perf_counter() - t0
+        torch.cuda.synchronize(dev)
+        res["cpu_baseline"] = {"value": n / dt, "unit": unit, "cores": threads, "kind": "port",
+                               "single_core": {"value": m1 / dt1, "unit": unit,
+                                               "sample": "pairing_batch of %d terms, 1 thread" % m1},
+                               "sample": "the whole 2^14-term pairing_batch, oracle shared loop split over %d "
+                                         "threads (orc_pairing_batch_mt), %.2f s wall" % (threads, dt),
+                               "parity_bit_exact": bool(np.array_equal(ref, gout.cpu().numpy().view(np.uint64))
+                                                        and int(gst.item()) == 0)}
+    elif args.workload == "g1mul":
         m = min(args.cpu_sample or 2048, n)
         threads = host_cpus()["usable"]
         ph, kh, oh = (t[:m].cpu().numpy().view(np.uint64) for t in (P, k2, out))
@@ -210,8 +244,6 @@ def other_workload(args, local_rank):
         res["cpu_baseline"] = {"value": m / dt, "unit": unit, "cores": threads, "kind": "port",
                                "sample": "%d G1*Fr of the bench inputs, oracle, %d threads" % (m, threads),
                                "parity_sample_bit_exact": bool(np.array_equal(ref, oh))}
-    else:
-        res["parity_bit_exact"] = bool(np.array_equal(ctx.pairing_batch(p, q), O.pairing_batch(p[:n], q[:n])))
     print(json.dumps(res), flush=True)
 
 

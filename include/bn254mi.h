@@ -97,6 +97,19 @@ int bn_pairing_batch(bn_ctx* ctx, const bn_g1* p, const bn_g2* q, size_t n, bn_g
  * mod.rs:609-640).  No final exponentiation.  BN_ERR_TO_AFFINE if any point is zero. */
 int bn_miller_loop_batch(bn_ctx* ctx, const bn_g2* q, const bn_g1* p, size_t n, bn_gt* out);
 
+/* Device-pointer forms (BASELINE config 5 with HBM-resident inputs): *d_out (one Gt
+ * on the device) = pairing_batch / miller_loop_batch of the n pairs, enqueued on
+ * `stream` without synchronizing.  The per-pair Miller values are reduced on the
+ * device (kernels_wide.hip) and pairing_batch's one final exponentiation runs on
+ * a 16-lane group.  Outcomes that depend on the data are written to *d_status
+ * (a device int, may be NULL) when the work completes: BN_OK, BN_ERR_TO_AFFINE
+ * (miller_loop_batch: a zero point, lib.rs:629-630; *d_out is then unspecified)
+ * or BN_ERR_FE_ZERO (pairing_batch: the reference panics; *d_out is zero). */
+int bn_pairing_batch_dev(bn_ctx* ctx, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, int* d_status,
+                         void* stream);
+int bn_miller_loop_batch_dev(bn_ctx* ctx, const bn_g2* d_q, const bn_g1* d_p, size_t n, bn_gt* d_out,
+                             int* d_status, void* stream);
+
 /* out[i] = Gt::final_exponentiation(f[i]) (lib.rs:598-600, fq12.rs:107-110);
  * ok[i] = 0 where f[i] == 0 (the reference returns None), out[i] then zero. */
 int bn_final_exponentiation_many(bn_ctx* ctx, const bn_gt* f, size_t n, bn_gt* out, uint8_t* ok);
@@ -179,8 +192,14 @@ int bn_gt_pow_many_dev(bn_ctx* ctx, const bn_gt* d_a, const bn_fr* d_k, size_t n
 /* enable HIP-event timing of each kernel phase of bn_pairing_many_dev (events are
  * recorded on the launch stream between the kernels) */
 int bn_set_phase_timing(bn_ctx* ctx, int enable);
+/* Batches of at most n elements run the final exponentiation on 16-lane groups
+ * (latency path, kernels_wide.hip); larger ones on the two-lane step machine
+ * (throughput path, k_fq12_vm).  Default 4096 or $BN254MI_FE_WIDE_MAX; results are
+ * identical either way.  On a multi-device context it applies to every device. */
+int bn_set_fe_wide_max(bn_ctx* ctx, size_t n);
 /* device milliseconds per phase since the last read: ms[0] k_prepare (to_affine +
- * G2 lines), ms[1] k_miller, ms[2] k_fq12_vm (final exponentiation), ms[3] k_fe_out;
+ * G2 lines), ms[1] k_miller, ms[2] final exponentiation (k_fq12_vm, or k_fe_wide for
+ * batches up to the wide threshold), ms[3] k_fe_out (0 with k_fe_wide);
  * *launches = launch sets measured */
 int bn_get_phase_times(bn_ctx* ctx, float ms[4], int* launches);
 

@@ -914,6 +914,69 @@ static void run_many(int kind, const void* a, const void* b, size_t n, void* out
     for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }
 void orc_pairing_many(const orc_g1* p, const orc_g2* q, size_t n, orc_fq12* out, int nthreads) { run_many(0, p, q, n, out, nthreads); }
+
+/* pairing_batch (mod.rs:904-926) on several threads: thread t runs the shared
+ * loop (miller_loop_multi) over its contiguous slice of the non-zero pairs, and
+ * the partial values are multiplied in slice order before the one final
+ * exponentiation.  Squaring is a ring homomorphism and Fq12 is commutative, so
+ * the product of the slices' loop values IS the single shared loop value:
+ * the result equals orc_pairing_batch's bit for bit (tests/test_oracle.py). */
+typedef struct {
+    const orc_g1* p;
+    const orc_g2* q;
+    size_t lo, hi;
+    fq12 f;
+    size_t live;
+} bjob;
+static void* run_bjob(void* arg) {
+    bjob* j = (bjob*)arg;
+    size_t n = j->hi - j->lo;
+    ell (*coeffs)[ORC_NUM_COEFFS] = malloc((n ? n : 1) * sizeof(*coeffs));
+    fe* px = malloc((n ? n : 1) * sizeof(fe));
+    fe* py = malloc((n ? n : 1) * sizeof(fe));
+    size_t m = 0;
+    for (size_t t = j->lo; t < j->hi; ++t) {
+        fe x, y;
+        g2aff qa;
+        if (g1_to_affine((const g1*)(const void*)&j->p[t], &x, &y)) continue;
+        if (g2_to_affine((const g2*)(const void*)&j->q[t], &qa.x, &qa.y)) continue;
+        px[m] = x;
+        py[m] = y;
+        precompute(&qa, coeffs[m]);
+        m++;
+    }
+    j->f = m ? miller_loop_multi(coeffs, px, py, m) : fq12_one();
+    j->live = m;
+    free(coeffs);
+    free(px);
+    free(py);
+    return NULL;
+}
+void orc_pairing_batch_mt(const orc_g1* p, const orc_g2* q, size_t n, orc_fq12* o, int nthreads) {
+    FP(0);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((size_t)nthreads > n) nthreads = n ? (int)n : 1;
+    pthread_t th[256];
+    bjob jobs[256];
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t].p = p;
+        jobs[t].q = q;
+        jobs[t].lo = n * t / nthreads;
+        jobs[t].hi = n * (t + 1) / nthreads;
+        pthread_create(&th[t], NULL, run_bjob, &jobs[t]);
+    }
+    fq12 f = fq12_one();
+    size_t live = 0;
+    for (int t = 0; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        f = fq12_mul(f, jobs[t].f);
+        live += jobs[t].live;
+    }
+    fq12 r = fq12_one();
+    if (live && fq12_final_exponentiation(f, &r)) abort();
+    ST(fq12, o, r);
+}
 void orc_g1_mul_many(const orc_g1* p, const orc_fe* k, size_t n, orc_g1* out, int nthreads) { run_many(1, p, k, n, out, nthreads); }
 void orc_g2_mul_many(const orc_g2* p, const orc_fe* k, size_t n, orc_g2* out, int nthreads) { run_many(2, p, k, n, out, nthreads); }
 

@@ -94,6 +94,8 @@ int  orc_miller_loop_batch(const orc_g2* q, const orc_g1* p, size_t n, orc_fq12*
 void orc_pairing_many(const orc_g1* p, const orc_g2* q, size_t n, orc_fq12* out, int nthreads);
 void orc_g1_mul_many(const orc_g1* p, const orc_fe* k, size_t n, orc_g1* out, int nthreads);
 void orc_g2_mul_many(const orc_g2* p, const orc_fe* k, size_t n, orc_g2* out, int nthreads);
+/* pairing_batch with the shared loop split over threads (same result as orc_pairing_batch) */
+void orc_pairing_batch_mt(const orc_g1* p, const orc_g2* q, size_t n, orc_fq12* out, int nthreads);
 
 
 /* ---- encodings / validation / decompression / Gt::pow ----

@@ -128,6 +128,7 @@ def lib():
             "orc_pairing_batch": ([vp, vp, sz, vp], None),
             "orc_miller_loop_batch": ([vp, vp, sz, vp], i),
             "orc_pairing_many": ([vp, vp, sz, vp, i], None),
+            "orc_pairing_batch_mt": ([vp, vp, sz, vp, i], None),
             "orc_g1_mul_many": ([vp, vp, sz, vp, i], None),
             "orc_g2_mul_many": ([vp, vp, sz, vp, i], None),
             "orc_fq_from_slice": ([vp, vp], i),
@@ -237,10 +238,15 @@ def pairing_many(p, q, nthreads=1):
     return out
 
 
-def pairing_batch(p, q):
+def pairing_batch(p, q, nthreads=None):
+    """pairing_batch (mod.rs:904-926); nthreads splits the shared loop over
+    threads (orc_pairing_batch_mt, the same result)."""
     p, q = _u64(p, 12), _u64(q, 24)
     out = np.zeros(48, dtype=np.uint64)
-    lib().orc_pairing_batch(_p(p), _p(q), p.shape[0], _p(out))
+    if nthreads is None:
+        lib().orc_pairing_batch(_p(p), _p(q), p.shape[0], _p(out))
+    else:
+        lib().orc_pairing_batch_mt(_p(p), _p(q), p.shape[0], _p(out), nthreads)
     return out
 
 

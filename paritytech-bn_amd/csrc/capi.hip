@@ -1,6 +1,7 @@
 // capi.hip -- host side of the C ABI (include/bn254mi.h): context, workspace,
 // chunking, the final-exponentiation step program, and kernel launches.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -29,6 +30,12 @@ int fail(bn_ctx* c, int code, const std::string& msg) {
             return fail(ctx, BN_ERR_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+#define RET_IF(x)              \
+    do {                       \
+        int r_ = (x);          \
+        if (r_) return r_;     \
+    } while (0)
+
 // order this call's device work after the workspace's previous user (see bn_ctx)
 int ws_acquire(bn_ctx* c, hipStream_t s) {
     if (c->ws_pending) HIPCHK(c, hipStreamWaitEvent(s, c->ws_event, 0));
@@ -50,6 +57,9 @@ int ws_drain(bn_ctx* c) {
 }
 
 constexpr int kFeSlots = 32;  // slot 0: Miller value, 1: easy-part result, 2..: temporaries
+// batches up to this size run the final exponentiation on the wide layout
+// (measured crossover; BN254MI_FE_WIDE_MAX or bn_set_fe_wide_max override)
+constexpr size_t kFeWideMaxDefault = 4096;
 
 size_t ws_bytes(size_t n) {
     return n * ((size_t)kCoeffFq * 9 * 4 + kPathLanes * (2 * 9 * 4 + 1) + (size_t)kFeSlots * kSlotWords * 4) + 64;
@@ -234,24 +244,134 @@ int miller_values(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int m
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
-// multiply the n lane-strided values of slot 0 together into lane 0
-int product_tree(bn_ctx* c, size_t n, hipStream_t s) {
-    for (size_t m = n; m > 1;) {
-        const size_t half = (m + 1) / 2;
-        k_fq12_product<<<grid_for(kPathLanes * half), kBlock, 0, s>>>(c->slots, n, m, half);
+// the region of Fq12 slot k of the workspace (room for c->cap split-layout elements)
+uint32_t* slot_region(bn_ctx* c, int k) { return c->slots + (size_t)k * kSlotWords * c->cap; }
+constexpr int kRegionA = 1, kRegionB = 2;  // ping-pong regions of the product reduction
+constexpr int kRegionParts = 3;            // per-chunk partial products
+constexpr int kRegionResult = 4;           // the final product (element 0, stride 1)
+constexpr size_t kWideElemsPerBlock = 2 * (kBlock / 16);  // k_fq12_reduce_wide: 32 elements per block
+
+// Multiply the n split-layout values of `in` (stride in_stride) together on
+// the wide layout (k_fq12_reduce_wide, a factor of 32 per launch) into element
+// out_base of `out` (stride out_stride).  `in` must not be a ping-pong region.
+int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, size_t n, uint32_t* out, size_t out_stride,
+                 size_t out_base, hipStream_t s) {
+    const uint32_t* src = in;
+    size_t sn = n, sstride = in_stride;
+    bool a = true;
+    for (;;) {
+        const size_t blocks = (sn + kWideElemsPerBlock - 1) / kWideElemsPerBlock;
+        if (blocks == 1) {
+            k_fq12_reduce_wide<<<1, kBlock, 0, s>>>(src, sstride, sn, out, out_stride, out_base);
+            HIPCHK(c, hipGetLastError());
+            return BN_OK;
+        }
+        uint32_t* dst = slot_region(c, a ? kRegionA : kRegionB);
+        k_fq12_reduce_wide<<<(unsigned)blocks, kBlock, 0, s>>>(src, sstride, sn, dst, blocks, 0);
         HIPCHK(c, hipGetLastError());
-        m = half;
+        src = dst;
+        sstride = blocks;
+        sn = blocks;
+        a = !a;
     }
-    return BN_OK;
 }
 
-// final exponentiation of the n values in slot 0 -> out (device Gt images)
-int run_fe(bn_ctx* c, size_t n, const uint8_t* flags, bn_gt* out, uint8_t* ok, hipStream_t s) {
+// final exponentiation of the n split-layout values of `f` (stride n) -> out
+// (device Gt images): the wide layout for small batches, else the step machine
+// (whose program reads and writes the slots from slot 0: f must be slot 0)
+int run_fe(bn_ctx* c, const uint32_t* f, size_t n, const uint8_t* flags, bn_gt* out, uint8_t* ok, hipStream_t s) {
+    if (n <= c->fe_wide_max) {
+        k_fe_wide<<<grid_for(16 * n), kBlock, 0, s>>>(f, n, n, out, ok, c->d_err);
+        HIPCHK(c, hipGetLastError());
+        return BN_OK;
+    }
+    if (f != c->slots) return fail(c, BN_ERR_INVALID_ARGUMENT, "internal: step-machine FE input must be slot 0");
     k_fq12_vm<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, n);
     HIPCHK(c, hipGetLastError());
     k_fe_out<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(c->slots, n, c->fe_out, flags, out, ok, c->d_err);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
+}
+
+// ---- pairing_batch / miller_loop_batch: segmented Miller loop + device reduction
+constexpr int kRegionSeg = 8;  // k_miller_seg output: segment g in region kRegionSeg + g
+
+// S segments of the 64 NAF digits (S doubles until S * n pairs fill about
+// 2^16 lane pairs, i.e. two waves per SIMD), cut so each carries about the same
+// work: a digit costs a squaring (36 Fq-mul) and a line (39), a nonzero digit
+// one more line, the last segment the two closing lines.
+SegPlan seg_plan(size_t n) {
+    SegPlan p{};
+    int S = 1;
+    while (S < kMaxSeg && (size_t)S * n < ((size_t)1 << 16)) S *= 2;
+    p.S = S;
+    auto cost = [](int d) { return 36 + 39 + (((kNafNonzero >> d) & 1u) ? 39 : 0); };
+    int total = 2 * 39;
+    for (int d = 0; d < BN_NAF_DIGITS; ++d) total += cost(d);
+    int g = 0, acc = 0;
+    p.lo[0] = 0;
+    for (int d = 0; d < BN_NAF_DIGITS; ++d) {
+        acc += cost(d);
+        if (g + 1 < S && acc * S >= total * (g + 1) && d + 1 < BN_NAF_DIGITS) {
+            p.hi[g] = d + 1;
+            p.lo[++g] = d + 1;
+        }
+    }
+    p.hi[g] = BN_NAF_DIGITS;
+    p.S = g + 1;
+    for (int k = 0; k < p.S; ++k)
+        p.idx[k] = p.lo[k] + __builtin_popcountll(kNafNonzero & ((p.lo[k] ? (1ull << p.lo[k]) : 1ull) - 1ull));
+    return p;
+}
+
+// Segment values of m <= kChunk device pairs (mode 0: a pair with a zero point
+// counts as one; mode 1: a zero point sets the BN_ERR_TO_AFFINE bit), each
+// segment reduced over the pairs into element g * nchunks + k (stride
+// S * nchunks) of `parts`
+int chunk_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int mode, const SegPlan& plan,
+                  uint32_t* parts, size_t nchunks, size_t k, hipStream_t s) {
+    k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags, c->d_err, mode);
+    HIPCHK(c, hipGetLastError());
+    k_miller_seg<<<grid_for(kPathLanes * plan.S * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
+                                                                       slot_region(c, kRegionSeg),
+                                                                       (size_t)kSlotWords * c->cap);
+    HIPCHK(c, hipGetLastError());
+    for (int g = 0; g < plan.S; ++g)
+        RET_IF(product_wide(c, slot_region(c, kRegionSeg + g), m, m, parts, plan.S * nchunks, g * nchunks + k, s));
+    return BN_OK;
+}
+// where chunk partials go: straight into the result region (element g, stride S)
+// for one chunk, else the parts region
+uint32_t* parts_region(bn_ctx* c, size_t nchunks) {
+    return nchunks == 1 ? slot_region(c, kRegionResult) : slot_region(c, kRegionParts);
+}
+// per segment, the chunk partials -> the result region; then the Horner
+// recombination (+ the final exponentiation for pairing_batch) into *d_out
+int finish_product(bn_ctx* c, const SegPlan& plan, size_t nchunks, int do_fe, bn_gt* d_out, hipStream_t s) {
+    if (nchunks > 1) {
+        uint32_t* parts = slot_region(c, kRegionParts);
+        for (int g = 0; g < plan.S; ++g)
+            RET_IF(product_wide(c, parts + 2 * g * nchunks, plan.S * nchunks, nchunks, slot_region(c, kRegionResult),
+                                plan.S, g, s));
+    }
+    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+// the whole product of n device pairs into *d_out; the caller holds the workspace
+int miller_product_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int mode, bn_gt* d_out,
+                       hipStream_t s) {
+    const size_t nchunks = (n + kChunk - 1) / kChunk;
+    const size_t m0 = n < kChunk ? n : kChunk;
+    const SegPlan plan = seg_plan(m0);
+    RET_IF(reserve(c, m0));
+    if (nchunks * plan.S > c->cap) return fail(c, BN_ERR_INVALID_ARGUMENT, "too many chunks");
+    uint32_t* parts = parts_region(c, nchunks);
+    for (size_t k = 0; k < nchunks; ++k) {
+        const size_t off = k * kChunk, m = (n - off) < kChunk ? (n - off) : kChunk;
+        RET_IF(chunk_product(c, d_p + off, d_q + off, m, mode, plan, parts, nchunks, k, s));
+    }
+    return finish_product(c, plan, nchunks, mode == 0, d_out, s);
 }
 
 int check_err(bn_ctx* c, hipStream_t s, int* out_bits) {
@@ -275,11 +395,6 @@ int clear_err(bn_ctx* c, hipStream_t s) {
                     "not available on a multi-device context; use bn_ctx_device()"); \
     std::lock_guard<std::mutex> lock_((ctx)->mu);      \
     HIPCHK(ctx, hipSetDevice((ctx)->device))
-#define RET_IF(x)              \
-    do {                       \
-        int r_ = (x);          \
-        if (r_) return r_;     \
-    } while (0)
 // host-buffer entry points: the lock for the whole call, and the context stream
 // ordered after the workspace's previous user
 #define CTX_GUARD_HOST(ctx)                \
@@ -358,6 +473,8 @@ int bn_ctx_create(int device, bn_ctx** out) {
     if (device < 0 || device >= count) return BN_ERR_INVALID_ARGUMENT;
     bn_ctx* c = new bn_ctx();
     c->device = device;
+    c->fe_wide_max = kFeWideMaxDefault;
+    if (const char* e = getenv("BN254MI_FE_WIDE_MAX")) c->fe_wide_max = (size_t)strtoull(e, nullptr, 10);
     Prog P;
     c->fe_out = (int)build_final_exp(P);
     P.finalize({(uint32_t)c->fe_out});
@@ -442,9 +559,15 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
         mark(1);
         k_miller<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, c->slots);
         mark(2);
-        k_fq12_vm<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, m);
-        mark(3);
-        k_fe_out<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->slots, m, c->fe_out, c->flags, d_out + off, nullptr, c->d_err);
+        if (m <= c->fe_wide_max) {  // latency: 16 lanes per element (kernels_wide.hip)
+            k_fe_wide<<<grid_for(16 * m), kBlock, 0, s>>>(c->slots, m, m, d_out + off, nullptr, c->d_err);
+            mark(3);
+        } else {
+            k_fq12_vm<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, m);
+            mark(3);
+            k_fe_out<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->slots, m, c->fe_out, c->flags, d_out + off, nullptr,
+                                                                 c->d_err);
+        }
         mark(4);
         HIPCHK(c, hipGetLastError());
         if (c->timing) c->ev_marks.push_back(ev);
@@ -508,55 +631,42 @@ int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* 
     return BN_OK;
 }
 
-// product of the Miller values of all pairs (mode 0: pairs with a zero point
-// contribute one; mode 1: a zero point is BN_ERR_TO_AFFINE) -> *result (host image)
-static int miller_product(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, int mode, bn_gt* result) {
+// The Miller product of n host pairs -> *out (host image), then pairing_batch's
+// final exponentiation when do_fe; mode 0 skips pairs with a zero point, mode 1
+// (miller_loop_batch) rejects them.  Chunks of kChunk pairs are staged in turn.
+// BN_ERR_TO_AFFINE / BN_ERR_FE_ZERO come from the device bits.
+static int batch_host(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, int mode, bool do_fe, bn_gt* out) {
     RET_IF(clear_err(c, c->stream));
-    std::vector<bn_gt> parts;
-    for (size_t off = 0; off < n; off += kChunk) {
-        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+    const size_t nchunks = (n + kChunk - 1) / kChunk;
+    const size_t m0 = n < kChunk ? n : kChunk;
+    const SegPlan plan = seg_plan(m0);
+    RET_IF(reserve(c, m0));
+    if (nchunks * plan.S > c->cap) return fail(c, BN_ERR_INVALID_ARGUMENT, "too many chunks");
+    uint32_t* parts = parts_region(c, nchunks);
+    for (size_t k = 0; k < nchunks; ++k) {
+        const size_t off = k * kChunk, m = (n - off) < kChunk ? (n - off) : kChunk;
         RET_IF(stage(c, m * (sizeof(bn_g1) + sizeof(bn_g2)) + sizeof(bn_gt)));
         bn_g1* dp = (bn_g1*)c->stage;
         bn_g2* dq = (bn_g2*)(dp + m);
-        bn_gt* dpart = (bn_gt*)(dq + m);
         HIPCHK(c, hipMemcpyAsync(dp, p + off, m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
-        RET_IF(reserve(c, m));
-        RET_IF(miller_values(c, dp, dq, m, mode, c->stream));
-        RET_IF(product_tree(c, m, c->stream));
-        k_gt_store<<<1, kBlock, 0, c->stream>>>(c->slots, 1, m, dpart);
-        HIPCHK(c, hipGetLastError());
-        bn_gt h;
-        HIPCHK(c, hipMemcpyAsync(&h, dpart, sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        parts.push_back(h);
+        RET_IF(chunk_product(c, dp, dq, m, mode, plan, parts, nchunks, k, c->stream));
+        if (k + 1 < nchunks) HIPCHK(c, hipStreamSynchronize(c->stream));  // the stage is reused
     }
+    bn_gt* d = (bn_gt*)c->stage;  // the stage holds at least one Gt past the inputs
+    RET_IF(finish_product(c, plan, nchunks, do_fe, d, c->stream));
+    HIPCHK(c, hipMemcpyAsync(out, d, sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
     int bits = 0;
     RET_IF(check_err(c, c->stream, &bits));
     if (bits & (1 << BN_ERR_TO_AFFINE)) return fail(c, BN_ERR_TO_AFFINE, "ToAffineConversion");
-    if (parts.size() == 1) {
-        *result = parts[0];
-        return BN_OK;
-    }
-    const size_t np = parts.size();
-    RET_IF(stage(c, (np + 1) * sizeof(bn_gt)));
-    bn_gt* d = (bn_gt*)c->stage;
-    HIPCHK(c, hipMemcpyAsync(d, parts.data(), np * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
-    RET_IF(reserve(c, np));
-    k_gt_load<<<grid_for(kPathLanes * np), kBlock, 0, c->stream>>>(d, np, c->slots);
-    RET_IF(product_tree(c, np, c->stream));
-    k_gt_store<<<1, kBlock, 0, c->stream>>>(c->slots, 1, np, d + np);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(result, d + np, sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (bits & (1 << BN_ERR_FE_ZERO)) return fail(c, BN_ERR_FE_ZERO, "miller loop cannot produce zero");
     return BN_OK;
 }
 
 // the Miller product of n host pairs on one single-device context (its lock held)
 int bn_internal_miller_product(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, int mode, bn_gt* result) {
     CTX_GUARD_HOST(c);
-    RET_IF(miller_product(c, p, q, n, mode, result));
-    return BN_OK;
+    return batch_host(c, p, q, n, mode, false, result);
 }
 
 void bn_internal_gt_one(bn_gt* out);
@@ -582,7 +692,7 @@ static int final_exp_host(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8
         HIPCHK(c, hipMemcpyAsync(din, f + off, m * sizeof(bn_gt), hipMemcpyHostToDevice, c->stream));
         k_gt_load<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(din, m, c->slots);
         HIPCHK(c, hipGetLastError());
-        RET_IF(run_fe(c, m, nullptr, dout, dok, c->stream));
+        RET_IF(run_fe(c, c->slots, m, nullptr, dout, dok, c->stream));
         HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
         if (ok) HIPCHK(c, hipMemcpyAsync(ok + off, dok, m, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -601,13 +711,7 @@ int bn_pairing_batch(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt*
         gt_one(out);
         return BN_OK;
     }
-    bn_gt prod;
-    RET_IF(miller_product(c, p, q, n, 0, &prod));
-    RET_IF(clear_err(c, c->stream));
-    int zero = 0;
-    RET_IF(final_exp_host(c, &prod, 1, out, nullptr, &zero));
-    if (zero) return fail(c, BN_ERR_FE_ZERO, "miller loop cannot produce zero");
-    return BN_OK;
+    return batch_host(c, p, q, n, 0, true, out);
 }
 
 int bn_miller_loop_batch(bn_ctx* c, const bn_g2* q, const bn_g1* p, size_t n, bn_gt* out) {
@@ -618,7 +722,48 @@ int bn_miller_loop_batch(bn_ctx* c, const bn_g2* q, const bn_g1* p, size_t n, bn
         gt_one(out);
         return BN_OK;
     }
-    return miller_product(c, p, q, n, 1, out);
+    return batch_host(c, p, q, n, 1, false, out);
+}
+
+// ---- device-pointer forms of pairing_batch / miller_loop_batch (config 5 with HBM-resident inputs)
+static int batch_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, int* d_status,
+                     int mode, hipStream_t s) {
+    if (!d_out || (n && (!d_p || !d_q))) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    RET_IF(reserve(c, n == 0 ? 1 : n < kChunk ? n : kChunk));
+    RET_IF(ws_acquire(c, s));
+    WsUse use{c, s};
+    HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), s));
+    if (n == 0) {  // pairing_batch: mod.rs:922-924; the shared loop starts from one (mod.rs:610)
+        static bn_gt one;
+        bn_internal_gt_one(&one);
+        HIPCHK(c, hipMemcpyAsync(d_out, &one, sizeof(bn_gt), hipMemcpyHostToDevice, s));
+    } else {
+        RET_IF(miller_product_dev(c, d_p, d_q, n, mode, d_out, s));
+    }
+    if (d_status) {
+        k_err_status<<<1, 64, 0, s>>>(c->d_err, d_status);
+        HIPCHK(c, hipGetLastError());
+    }
+    return BN_OK;
+}
+int bn_pairing_batch_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, int* d_status,
+                         void* stream) {
+    CTX_GUARD(c);
+    return batch_dev(c, d_p, d_q, n, d_out, d_status, 0, pick(c, stream));
+}
+int bn_miller_loop_batch_dev(bn_ctx* c, const bn_g2* d_q, const bn_g1* d_p, size_t n, bn_gt* d_out, int* d_status,
+                             void* stream) {
+    CTX_GUARD(c);
+    return batch_dev(c, d_p, d_q, n, d_out, d_status, 1, pick(c, stream));
+}
+int bn_set_fe_wide_max(bn_ctx* c, size_t n) {
+    if (c && !c->subs.empty()) {
+        for (bn_ctx* d : c->subs) RET_IF(bn_set_fe_wide_max(d, n));
+        return BN_OK;
+    }
+    CTX_GUARD(c);
+    c->fe_wide_max = n;
+    return BN_OK;
 }
 
 int bn_final_exponentiation_many(bn_ctx* c, const bn_gt* f, size_t n, bn_gt* out, uint8_t* ok) {

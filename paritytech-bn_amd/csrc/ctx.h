@@ -26,6 +26,10 @@ struct bn_ctx {
     std::vector<std::array<hipEvent_t, 5>> ev_marks;
     int fe_steps = 0;
     int fe_out = 0;
+    // batches of at most this many elements run the final exponentiation on the
+    // wide layout (kernels_wide.hip, 16 lanes per element: latency) instead of
+    // the step machine (k_fq12_vm, 2 lanes per element: throughput)
+    size_t fe_wide_max = 0;
     int* d_err = nullptr;
     // staging for host-buffer calls (device)
     size_t stage_bytes = 0;

@@ -1,0 +1,338 @@
+// fq12_wide.h -- one Fq12 spread over twelve lanes ("wide" layout), for the
+// latency-bound end of the pairing path: the final exponentiation of a handful
+// of values (pairing_batch, small batches) and the product reduction of
+// pairing_batch / miller_loop_batch (mod.rs:609-640, 904-926).
+//
+// Why: the batch layout (fq2_split.h) runs one Fq12 on two lanes, so a single
+// final exponentiation is one lane pair doing ~17k dependent Fq products --
+// 2.9 ms on an otherwise idle GPU (profiles/r2f_kernel_stats_product.csv).
+// Here a group of 16 lanes holds one element: lane 2e + c holds coordinate c
+// of the Fq2 coefficient of w^e (Fq12 = Fq2[w]/(w^6 - xi); w^e is c0.c(e/2)
+// for even e and c1.c((e-1)/2) for odd e, fq12.rs:52-55).  Lanes 12..15 mirror
+// lanes 10..11 (e = 5) and are never read.  A product is a schoolbook sum over
+// the six coefficients of each operand, so every lane accumulates twelve digit
+// products into one set of column sums and reduces ONCE: out_e = sum_i a'_i *
+// b_(e-i mod 6) with a'_i = xi*a_i when i > e (w^6 = xi).  Operands are
+// exchanged through a per-group LDS area (each lane writes its coordinate,
+// then reads the ones it needs; a wave runs its LDS operations in order, so
+// the exchange needs no barrier).  Within a lane pair the two-lane Fq2
+// operations of fq2_split.h apply unchanged (partner over DPP).
+//
+// Bit-exactness: every operation computes the field value of the reference
+// operation it replaces (schoolbook vs Karatsuba is a ring identity; the
+// cyclotomic squaring is the reference's Granger-Scott formula, fq12.rs:198-247),
+// and images are canonicalized at the boundary as everywhere else.
+#pragma once
+#include "kernels.h"
+
+namespace bn {
+static_assert(BN_SPLIT, "fq12_wide.h builds on the two-lane Fq2 of fq2_split.h");
+
+constexpr int kWLanes = 16;                         // lanes per element (12 hold coordinates)
+constexpr int kWSlot = 12;                          // words per LDS slot: one Fq, 48 B aligned
+constexpr int kWArr = kWLanes * kWSlot;             // words of one operand array of a group
+constexpr int kWArrs = 4;                           // operand arrays per group
+constexpr int kWGroupWords = kWArrs * kWArr;        // 3 KB per group
+constexpr int kWGroups = kBlock / kWLanes;          // 16 groups per 256-thread block
+__shared__ uint32_t g_wide[kWGroups * kWGroupWords];  // 48 KB
+
+// this lane's place in its group
+struct WL {
+    uint32_t* gb;  // the group's LDS operand area
+    int l;         // lane in group, 0..15 (LDS slot)
+    int e;         // w exponent of the coefficient (lanes 12..15 mirror e = 5)
+    int c;         // coordinate: 0 = c0, 1 = c1 of the Fq2 coefficient
+};
+__device__ __forceinline__ WL wl() {
+    const int t = (int)threadIdx.x;
+    WL w;
+    w.l = t & (kWLanes - 1);
+    w.e = (w.l >> 1) < 5 ? (w.l >> 1) : 5;
+    w.c = t & 1;
+    w.gb = g_wide + (t / kWLanes) * kWGroupWords;
+    return w;
+}
+// Gt image index of this lane's coordinate (c_i.c_j.c_k at 6i + 2j + k)
+__device__ __forceinline__ int w_gt_index(const WL& w) { return 6 * (w.e & 1) + 2 * (w.e >> 1) + w.c; }
+// tower index of the lane's Fq2 (c_i.c_j at 3i + j): the slot j of the
+// lane-strided split layout (kernels.h st_fq12/ld_fq12)
+__device__ __forceinline__ int w_tower_index(const WL& w) { return 3 * (w.e & 1) + (w.e >> 1); }
+
+template <int K>
+__device__ __forceinline__ void w_put(uint32_t* arr, int slot, const Fq<K>& x) {
+    static_assert(kl(K) == 1, "w_put: normalized digits");
+    uint32_t* p = arr + slot * kWSlot;
+    *(uint4*)p = make_uint4(x.v[0], x.v[1], x.v[2], x.v[3]);
+    *(uint4*)(p + 4) = make_uint4(x.v[4], x.v[5], x.v[6], x.v[7]);
+    p[8] = x.v[8];
+}
+template <int K>
+__device__ __forceinline__ Fq<K> w_get(const uint32_t* arr, int slot) {
+    const uint32_t* p = arr + slot * kWSlot;
+    const uint4 a = *(const uint4*)p, b = *(const uint4*)(p + 4);
+    return Fq<K>{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, p[8]}};
+}
+// the writes above are complete before any lane reads (and the compiler keeps order)
+__device__ __forceinline__ void w_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// normalized, value <= 2p
+template <int K>
+__device__ __forceinline__ Fq<2> w_narrow(const Fq<K>& a) {
+    if constexpr (kv(K) <= 2) return widen<2>(fq_norm(a)); else return fq_fold(a);
+}
+
+// ---------------------------------------------------------------- column accumulator
+// sum of digit products of several Fq products in 17 64-bit columns, carried
+// between batches and reduced once (Montgomery, R = 2^261)
+struct Acc {
+    uint64_t c[17];
+};
+template <int A, int B>
+__device__ __forceinline__ void acc_mad(Acc& t, const Fq<A>& x, const Fq<B>& y) {
+    static_assert(kl(A) == 1 && kl(B) == 1, "acc_mad: normalized operands");
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) t.c[i + j] += (uint64_t)x.v[i] * y.v[j];
+}
+__device__ __forceinline__ void acc_carry(Acc& t) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        t.c[k + 1] += t.c[k] >> 29;
+        t.c[k] &= M29;
+    }
+}
+// REDC of carried columns holding a value <= U * p^2 (U = sum of the operand
+// bound products): result <= (U*p/2^261 + 1) * p
+template <int U>
+__device__ __forceinline__ auto acc_redc(Acc& t) {
+    constexpr int BO = 1 + (int)(((long long)U * 5908 + 999999) / 1000000);
+    Fq<BO> r;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        const uint32_t m = ((uint32_t)t.c[k] * BN_PINV29) & M29;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) t.c[k + j] += (uint64_t)m * kP29.v[j];
+        t.c[k + 1] += t.c[k] >> 29;
+    }
+#pragma unroll
+    for (int k = 9; k < 16; ++k) {
+        t.c[k + 1] += t.c[k] >> 29;
+        r.v[k - 9] = (uint32_t)t.c[k] & M29;
+    }
+    r.v[7] = (uint32_t)t.c[16] & M29;
+    r.v[8] = (uint32_t)(t.c[16] >> 29);
+    return r;
+}
+
+// ---------------------------------------------------------------- operations
+// this lane's coordinate of xi * (the lane pair's Fq2), xi = 9 + u (fq2.rs:19-34)
+template <int K>
+__device__ __forceinline__ Fq<2> w_xi(const Fq<K>& a) { return fq2_fold(fq2_mul_xi(Fq2<K>{a})).c; }
+
+// a * b (fq12.rs:319-327), schoolbook over the w-basis, one reduction per lane
+__device__ __noinline__ Fq<2> w12_mul(Fq<2> a, Fq<2> b) {
+    const WL w = wl();
+    uint32_t* A_ = w.gb;
+    uint32_t* X_ = w.gb + kWArr;
+    uint32_t* B_ = w.gb + 2 * kWArr;
+    uint32_t* N_ = w.gb + 3 * kWArr;
+    w_put(A_, w.l, a);
+    w_put(X_, w.l, w_xi(a));
+    w_put(B_, w.l, b);
+    w_put(N_, w.l, fq_neg(b));
+    w_sync();
+    Acc t = {};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const bool wrap = i > w.e;                  // a_i * b_(e-i+6) * w^6, w^6 = xi
+        const int j = wrap ? w.e - i + 6 : w.e - i;
+        const uint32_t* src = wrap ? X_ : A_;
+        const Fq<2> x0 = w_get<2>(src, 2 * i), x1 = w_get<2>(src, 2 * i + 1);
+        // c0: x0*b0 - x1*b1, c1: x0*b1 + x1*b0
+        const Fq<2> yo = w_get<2>(B_, 2 * j + w.c);
+        const Fq<2> yx = w_get<2>(w.c ? B_ : N_, 2 * j + 1 - w.c);
+        acc_mad(t, x0, yo);
+        acc_mad(t, x1, yx);
+        if (i == 2) acc_carry(t);  // six normalized products per batch keep columns < 2^64
+    }
+    acc_carry(t);
+    return acc_redc<12 * 2 * 2>(t);
+}
+
+// Granger-Scott cyclotomic squaring (fq12.rs:198-247).  Pairs (z0,z1), (z2,z3),
+// (z4,z5) are the coefficient pairs (w^k, w^(k+3)), k = 0, 1, 2.  Lane pair e < 3
+// computes tmp_e = x*y for pair k = e; lane pair e >= 3 computes
+// (x + y)(xi*y + x) for pair k = e - 3; then every lane forms its output
+// coordinate from them: t0 = P3 - P0 - xi*P0 etc. as in the reference.
+__device__ __noinline__ Fq<2> w12_cyc(Fq<2> a) {
+    const WL w = wl();
+    uint32_t* A_ = w.gb;
+    uint32_t* X_ = w.gb + kWArr;
+    uint32_t* P_ = w.gb + 2 * kWArr;
+    uint32_t* Q_ = w.gb + 3 * kWArr;
+    w_put(A_, w.l, a);
+    w_put(X_, w.l, w_xi(a));
+    w_sync();
+    const bool hi = w.e >= 3;
+    const int k = hi ? w.e - 3 : w.e;
+    const Fq<2> x0 = w_get<2>(A_, 2 * k), x1 = w_get<2>(A_, 2 * k + 1);
+    const Fq<2> y0 = w_get<2>(A_, 2 * k + 6), y1 = w_get<2>(A_, 2 * k + 7);
+    const Fq<2> xy0 = w_get<2>(X_, 2 * k + 6), xy1 = w_get<2>(X_, 2 * k + 7);  // xi * y
+    // U = hi ? x + y : x,  V = hi ? xi*y + x : y
+    const Fq<4> u0 = fq_norm(fq_pick(hi, fq_add(x0, y0), x0));
+    const Fq<4> u1 = fq_norm(fq_pick(hi, fq_add(x1, y1), x1));
+    const Fq<4> v0 = fq_norm(fq_pick(hi, fq_add(xy0, x0), y0));
+    const Fq<4> v1 = fq_norm(fq_pick(hi, fq_add(xy1, x1), y1));
+    // lane c of U*V: c0 = u0 v0 - u1 v1, c1 = u0 v1 + u1 v0
+    const Fq<4> vo = fq_select(w.c != 0, v1, v0);
+    const Fq<4> vx = fq_select(w.c != 0, v0, fq_neg(v1));
+    const auto p = fq_dot2(u0, vo, u1, vx);
+    const Fq<2> pn = w_narrow(p);
+    w_put(P_, w.l, pn);
+    w_put(Q_, w.l, w_xi(pn));
+    w_sync();
+    // even e (z0, z4, z3 = w^0, w^2, w^4): 3*(P_(k+3) - P_k - xi*P_k) - 2*a with k = e/2
+    // odd e: z1 = w^3: 6*P_0 + 2a;  z5 = w^5: 6*P_1 + 2a;  z2 = w^1: 6*xi*P_2 + 2a
+    const int ka = w.e >> 1;
+    const Fq<2> pu = w_get<2>(P_, 2 * (ka + 3) + w.c), pv = w_get<2>(P_, 2 * ka + w.c);
+    const Fq<2> pw = w_get<2>(Q_, 2 * ka + w.c);
+    const Fq<2> px = w.e == 1 ? w_get<2>(Q_, 4 + w.c) : w_get<2>(P_, (w.e >= 3 ? w.e - 3 : 0) + w.c);
+    const auto ta = fq_norm(fq_sub(fq_sub(pu, pv), pw));
+    const Fq<2> oa = fq_fold(fq_sub(fq_add(ta, fq_add(ta, ta)), fq_dbl(a)));
+    const auto tb = fq_dbl(px);
+    const Fq<2> ob = fq_fold(fq_add(fq_add(tb, fq_add(tb, tb)), fq_dbl(a)));
+    return fq_select((w.e & 1) == 0, oa, ob);
+}
+
+// unitary inverse (fq12.rs:126-128): the w^odd coefficients negate
+__device__ __forceinline__ Fq<2> w12_conj(const Fq<2>& a) {
+    const WL w = wl();
+    return fq_select((w.e & 1) != 0, fq_neg(a), a);
+}
+
+// frobenius_map(K) (fq12.rs:112-119, fq6.rs:125-131): coefficient c_i.c_j maps
+// to conj^K(x) * fq6_frob_c_j(K) [* fq12_frob_c1(K) for i = 1]
+template <int K>
+__device__ __noinline__ Fq<2> w12_frob(Fq<2> a) {
+    const WL w = wl();
+    const int j = w.e >> 1, i = w.e & 1;
+    Fq2<2> x = {a};
+    if constexpr (K & 1) x = widen<2>(fq2_conj(x));
+    const Fq2<1> c6 = fq2_select(j == 1, fq6_frob_c1(K), fq2_select(j == 2, fq6_frob_c2(K), fq2_one()));
+    const Fq2<1> c12 = fq2_select(i == 1, fq12_frob_c1(K), fq2_one());
+    const auto y = fq2_mul(x, c6);
+    return w_narrow(fq2_mul(y, c12).c);
+}
+
+// inverse (fq12.rs:305-313): every lane pair gathers the element into the
+// two-lane layout, inverts it there (one Fermat inversion of an Fq), and keeps
+// its own coefficient
+__device__ __noinline__ Fq<2> w12_inv(Fq<2> a) {
+    const WL w = wl();
+    uint32_t* A_ = w.gb;
+    w_put(A_, w.l, a);
+    w_sync();
+    auto g = [&](int e) { return Fq2<2>{w_get<2>(A_, 2 * e + w.c)}; };
+    const Fq12<2> f = {{g(0), g(2), g(4)}, {g(1), g(3), g(5)}};
+    const Fq12<2> r = fq12_fold(fq12_inv(f));
+    Fq<2> o = r.c0.c0.c;
+    o = fq_select(w.e == 1, r.c1.c0.c, o);
+    o = fq_select(w.e == 2, r.c0.c1.c, o);
+    o = fq_select(w.e == 3, r.c1.c1.c, o);
+    o = fq_select(w.e == 4, r.c0.c2.c, o);
+    o = fq_select(w.e == 5, r.c1.c2.c, o);
+    return o;
+}
+
+// every coordinate of the group's element is zero
+__device__ __forceinline__ bool w12_is_zero(const Fq<2>& a) {
+    const uint64_t m = __ballot(fq_is_zero(a));
+    const int sh = (int)(threadIdx.x & 63u) & ~(kWLanes - 1);
+    return ((m >> sh) & 0xfffull) == 0xfffull;
+}
+
+// ---------------------------------------------------------------- final exponentiation
+// exp_by_neg_z (fq12.rs:121-124): conj(x^u), u = 4965661367192848881, by signed
+// width-4 windows (x^-d = conj(x^d) in the cyclotomic subgroup, where the final
+// exponentiation applies it); the digit table is planned at compile time.
+struct ZWin {
+    int n = 0;
+    int8_t d[32] = {};
+    uint8_t run[32] = {};  // squarings before digit t (run[0]: unused)
+    uint8_t tail = 0;      // squarings after the last digit
+};
+constexpr ZWin z_windows() {
+    ZWin w;
+    uint64_t u = 4965661367192848881ull;
+    int dd[32] = {}, pp[32] = {}, n = 0;
+    for (int pos = 0; u; ++pos, u >>= 1) {
+        if (!(u & 1)) continue;
+        int z = (int)(u & 15);
+        if (z >= 8) z -= 16;
+        dd[n] = z;
+        pp[n] = pos;
+        ++n;
+        u -= (uint64_t)(int64_t)z;
+    }
+    w.n = n;
+    for (int t = 0; t < n; ++t) {  // top digit first
+        w.d[t] = (int8_t)dd[n - 1 - t];
+        w.run[t] = (uint8_t)(t ? pp[n - t] - pp[n - 1 - t] : 0);
+    }
+    w.tail = (uint8_t)pp[0];
+    return w;
+}
+constexpr ZWin kZWin = z_windows();
+
+__device__ __noinline__ Fq<2> w12_exp_by_neg_z(Fq<2> x) {
+    const Fq<2> x2 = w12_cyc(x);
+    const Fq<2> x3 = w12_mul(x, x2);
+    const Fq<2> x5 = w12_mul(x3, x2);
+    const Fq<2> x7 = w12_mul(x5, x2);
+    auto pick = [&](int d) {
+        const int m = d < 0 ? -d : d;
+        Fq<2> y = m == 1 ? x : m == 3 ? x3 : m == 5 ? x5 : x7;
+        return d < 0 ? w12_conj(y) : y;
+    };
+    Fq<2> r = pick(kZWin.d[0]);
+#pragma unroll 1
+    for (int t = 1; t < kZWin.n; ++t) {
+#pragma unroll 1
+        for (int s = 0; s < kZWin.run[t]; ++s) r = w12_cyc(r);
+        r = w12_mul(r, pick(kZWin.d[t]));
+    }
+#pragma unroll 1
+    for (int s = 0; s < kZWin.tail; ++s) r = w12_cyc(r);
+    return w12_conj(r);
+}
+
+// final_exponentiation (fq12.rs:107-110) of a nonzero f: first chunk
+// (fq12.rs:62-73) and last chunk (fq12.rs:75-105) in the reference's order
+__device__ __noinline__ Fq<2> w12_final_exp(Fq<2> f) {
+    const Fq<2> b0 = w12_inv(f);
+    const Fq<2> c0 = w12_mul(w12_conj(f), b0);
+    const Fq<2> d0 = w12_frob<2>(c0);
+    const Fq<2> s = w12_mul(d0, c0);
+    const Fq<2> a = w12_exp_by_neg_z(s);
+    const Fq<2> b = w12_cyc(a);
+    const Fq<2> c = w12_cyc(b);
+    const Fq<2> d = w12_mul(c, b);
+    const Fq<2> e = w12_exp_by_neg_z(d);
+    const Fq<2> f1 = w12_cyc(e);
+    const Fq<2> g = w12_exp_by_neg_z(f1);
+    const Fq<2> j = w12_mul(w12_conj(g), e);
+    const Fq<2> k = w12_mul(j, w12_conj(d));
+    const Fq<2> l = w12_mul(k, b);
+    const Fq<2> m = w12_mul(k, e);
+    const Fq<2> n = w12_mul(s, m);
+    const Fq<2> o = w12_frob<1>(l);
+    const Fq<2> p = w12_mul(o, n);
+    const Fq<2> q = w12_frob<2>(k);
+    const Fq<2> r = w12_mul(q, p);
+    const Fq<2> t = w12_mul(w12_conj(s), l);
+    const Fq<2> u = w12_frob<3>(t);
+    return w12_mul(u, r);
+}
+
+}  // namespace bn

@@ -413,7 +413,23 @@ inline void vm_step(uint32_t out[2], uint32_t op, uint32_t d, uint32_t a, uint32
     out[1] = k | (flags << 8);
 }
 
+// Segments of the Miller loop's 64 NAF digits (k_miller_seg / k_horner_wide):
+// segment s covers digits [lo[s], hi[s]) and starts at line coefficient idx[s]
+constexpr int kMaxSeg = 8;
+struct SegPlan {
+    int S;
+    int lo[kMaxSeg], hi[kMaxSeg], idx[kMaxSeg];
+};
+
 // ---------------------------------------------------------------- kernels
+__global__ void __launch_bounds__(kBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
+                                                       const uint32_t* __restrict__ paff,
+                                                       const uint8_t* __restrict__ flags, size_t n, SegPlan plan,
+                                                       uint32_t* __restrict__ out, size_t seg_words);
+// out = Horner recombination of the S segment values g[s] (element s, stride S, split
+// layout): x = g0; x = x^(2^len_s) * g_s; then the final exponentiation when do_fe
+__global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, SegPlan plan, int do_fe,
+                                                        bn_gt* __restrict__ out, int* __restrict__ err);
 __global__ void __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
                           uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
                           int* __restrict__ err, int mode);
@@ -423,6 +439,14 @@ __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__
 __global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot, const uint8_t* __restrict__ flags,
                          bn_gt* __restrict__ out, uint8_t* __restrict__ ok, int* __restrict__ err);
 __global__ void __launch_bounds__(kBlock) k_fq12_product(uint32_t* __restrict__ f, size_t stride, size_t m, size_t half);
+// kernels_wide.hip (fq12_wide.h): final exponentiation and product reduction on 16-lane groups
+__global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__ f, size_t stride, size_t n,
+                                                    bn_gt* __restrict__ out, uint8_t* __restrict__ ok,
+                                                    int* __restrict__ err);
+__global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
+                                                             size_t n, uint32_t* __restrict__ out,
+                                                             size_t out_stride, size_t out_base);
+__global__ void __launch_bounds__(kBlock) k_err_status(const int* __restrict__ err, int* __restrict__ status);
 __global__ void __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g, size_t n, uint32_t* __restrict__ f);
 __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict__ f, size_t n, size_t stride, bn_gt* __restrict__ g);
 __global__ void __launch_bounds__(kBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g1* __restrict__ out);

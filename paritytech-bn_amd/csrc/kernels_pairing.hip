@@ -96,6 +96,31 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* 
     st_fq12(f_out, nl, l, f);
 }
 
+// Miller loop in segments (pairing_batch / miller_loop_batch with fewer pairs
+// than fill the GPU): lane pair (segment s, pair i) -- segment-major, so a wave
+// reads consecutive pairs' coefficients -- computes pair i's loop over the
+// segment's digits (pairing.h miller_segment) into element i of
+// out + s * seg_words.  Segment values of a pair with a zero point are one.
+__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
+                                                                   const uint32_t* __restrict__ paff,
+                                                                   const uint8_t* __restrict__ flags, size_t n,
+                                                                   SegPlan plan, uint32_t* __restrict__ out,
+                                                                   size_t seg_words) {
+    fold_table_init();
+    const size_t l = lane_id(), pr = l / kL, nl = kL * n;
+    if (pr >= (size_t)plan.S * n) return;
+    const int s = (int)(pr / n);
+    const size_t lt = (pr % n) * kL + (l % kL);  // the pair's lane in the per-pair arrays
+    const Fq<2> px = ld_fq<2>(paff, nl, lt, 0);
+    const Fq<2> py = ld_fq<2>(paff, nl, lt, 1);
+    Fq12<kF> f = miller_segment(px, py, plan.lo[s], plan.hi[s], plan.idx[s], [&](int k) {
+        return Ell{ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 0), ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 2),
+                   ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 4)};
+    });
+    if (flags[lt]) f = widen<kF>(fq12_one());
+    st_fq12(out + (size_t)s * seg_words, nl, lt, f);
+}
+
 }  // namespace bn
 
 BN_EXPORT_FOLD_CHECK(pairing)

@@ -63,6 +63,27 @@ BN_INLINE Fq12<kF> miller_loop(const Fq<PB>& px, const Fq<PB>& py, Line&& line) 
     return f;
 }
 
+// One segment of the Miller loop: digits [lo, hi) starting from f = one, with
+// line coefficients from index `idx` on; the last segment (hi == 64) also
+// applies the two lines after the loop.  Running the loop over digits
+// [0, 64) in segments g_0 .. g_(S-1) gives f = (..((g_0)^(2^len_1) g_1)^(2^len_2)
+// ..) g_(S-1): squaring is a ring homomorphism, so the Horner recombination
+// (kernels_wide.hip k_horner_wide) reproduces mod.rs:579-640 exactly.
+template <int PB, typename Line>
+BN_INLINE Fq12<kF> miller_segment(const Fq<PB>& px, const Fq<PB>& py, int lo, int hi, int idx, Line&& line) {
+    Fq12<kF> f = widen<kF>(fq12_one());
+#pragma unroll 1
+    for (int i = lo; i < hi; ++i) {
+        f = apply_line(narrow12<kF>(fq12_sqr(f)), line(idx++), px, py);
+        if ((kNafNonzero >> i) & 1u) f = apply_line(f, line(idx++), px, py);
+    }
+    if (hi == BN_NAF_DIGITS) {
+        f = apply_line(f, line(idx++), px, py);
+        f = apply_line(f, line(idx), px, py);
+    }
+    return f;
+}
+
 // ---------------------------------------------------------------- final exponentiation
 BN_INLINE Fq12<kF> mul12(const Fq12<kF>& a, const Fq12<kF>& b) { return narrow12<kF>(fq12_mul(a, b)); }
 BN_INLINE Fq12<kF> cyc_sqr(const Fq12<kF>& a) { return narrow12<kF>(fq12_cyclotomic_sqr(a)); }

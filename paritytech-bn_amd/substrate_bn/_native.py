@@ -34,6 +34,7 @@ EXPORTS = [
     "bn_g2_affine_new_many", "bn_g2_affine_new_many_dev", "bn_g1_from_compressed_many", "bn_g2_from_compressed_many",
     "bn_g1_from_compressed_many_dev", "bn_g2_from_compressed_many_dev", "bn_gt_pow_many", "bn_gt_pow_many_dev",
     "bn_ctx_create_multi", "bn_ctx_num_devices", "bn_ctx_device", "bn_shard_range", "bn_pairing_many_allgather_dev",
+    "bn_pairing_batch_dev", "bn_miller_loop_batch_dev", "bn_set_fe_wide_max",
 ]
 
 # per-element status (bn_elem_status)
@@ -109,6 +110,9 @@ def load():
         "bn_ctx_device": ([vp, i], vp),
         "bn_shard_range": ([sz, i, i, ctypes.POINTER(sz), ctypes.POINTER(sz)], None),
         "bn_pairing_many_allgather_dev": ([vp, vp, vp, sz, vp, vp], i),
+        "bn_pairing_batch_dev": ([vp, vp, vp, sz, vp, vp, vp], i),
+        "bn_miller_loop_batch_dev": ([vp, vp, vp, sz, vp, vp, vp], i),
+        "bn_set_fe_wide_max": ([vp, sz], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -271,6 +275,16 @@ class Context:
 
     def g2_mul_many_dev(self, d_p, d_k, n, d_out, stream=None):
         self._check(self._L.bn_g2_mul_many_dev(self._h, d_p, d_k, n, d_out, stream))
+
+    def pairing_batch_dev(self, d_p, d_q, n, d_out, d_status=None, stream=None):
+        self._check(self._L.bn_pairing_batch_dev(self._h, d_p, d_q, n, d_out, d_status, stream))
+
+    def miller_loop_batch_dev(self, d_q, d_p, n, d_out, d_status=None, stream=None):
+        self._check(self._L.bn_miller_loop_batch_dev(self._h, d_q, d_p, n, d_out, d_status, stream))
+
+    def set_fe_wide_max(self, n):
+        """Batches of at most n elements use the 16-lane final exponentiation (latency path)."""
+        self._check(self._L.bn_set_fe_wide_max(self._h, n))
 
     def set_phase_timing(self, enable=True):
         self._check(self._L.bn_set_phase_timing(self._h, 1 if enable else 0))

@@ -163,3 +163,24 @@ def test_pairing_batch_semantics():
     # miller_loop_batch refuses a zero point (lib.rs:629-630)
     rc, _ = O.miller_loop_batch(q, p2)
     assert rc == 1
+
+
+def test_pairing_batch_threads_match_shared_loop():
+    """The threaded pairing_batch (the CPU baseline of config 5) splits the shared
+    loop (mod.rs:609-640) into per-thread slices whose values are multiplied in
+    order: the same Gt as the single shared loop, zero pairs and empty slices included."""
+    p, q, _, _ = O.random_pairs(9, seed=41)
+    p[4] = 0
+    p[4, 4:8] = O.canon_to_mont_array([1])      # G1::zero() inside one slice
+    ref = O.pairing_batch(p, q)
+    for t in (1, 2, 3, 4, 9, 16):
+        assert np.array_equal(O.pairing_batch(p, q, nthreads=t), ref), t
+    # a slice with nothing but zero points, and all pairs skipped -> Gt::one()
+    pz = p.copy()
+    pz[:5] = 0
+    pz[:5, 4:8] = O.canon_to_mont_array([1])
+    assert np.array_equal(O.pairing_batch(pz, q, nthreads=3), O.pairing_batch(pz, q))
+    gt_one = O.canon_to_mont_array([1] + [0] * 11)
+    pz[:] = 0
+    pz[:, 4:8] = O.canon_to_mont_array([1])
+    assert np.array_equal(O.pairing_batch(pz, q, nthreads=4), gt_one)
