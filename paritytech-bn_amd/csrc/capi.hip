@@ -251,27 +251,32 @@ constexpr int kRegionParts = 3;            // per-chunk partial products
 constexpr int kRegionResult = 4;           // the final product (element 0, stride 1)
 constexpr size_t kWideElemsPerBlock = 2 * (kBlock / 16);  // k_fq12_reduce_wide: 32 elements per block
 
-// Multiply the n split-layout values of `in` (stride in_stride) together on
-// the wide layout (k_fq12_reduce_wide, a factor of 32 per launch) into element
-// out_base of `out` (stride out_stride).  `in` must not be a ping-pong region.
-int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, size_t n, uint32_t* out, size_t out_stride,
-                 size_t out_base, hipStream_t s) {
+// Multiply each of `sets` sets of n split-layout values together on the wide
+// layout (k_fq12_reduce_wide, a factor of 32 per launch, all sets in one
+// launch): set y is elements y * in_set + [0, n) of `in` (stride in_stride),
+// its product goes to element out_base + y * out_set of `out` (stride
+// out_stride).  `in` must not be a ping-pong region.
+int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, size_t n, size_t in_set, int sets, uint32_t* out,
+                 size_t out_stride, size_t out_base, size_t out_set, hipStream_t s) {
     const uint32_t* src = in;
-    size_t sn = n, sstride = in_stride;
+    size_t sn = n, sstride = in_stride, sset = in_set;
     bool a = true;
     for (;;) {
         const size_t blocks = (sn + kWideElemsPerBlock - 1) / kWideElemsPerBlock;
         if (blocks == 1) {
-            k_fq12_reduce_wide<<<1, kBlock, 0, s>>>(src, sstride, sn, out, out_stride, out_base);
+            k_fq12_reduce_wide<<<dim3(1, sets), kBlock, 0, s>>>(src, sstride, sn, sset, out, out_stride, out_base,
+                                                                out_set);
             HIPCHK(c, hipGetLastError());
             return BN_OK;
         }
         uint32_t* dst = slot_region(c, a ? kRegionA : kRegionB);
-        k_fq12_reduce_wide<<<(unsigned)blocks, kBlock, 0, s>>>(src, sstride, sn, dst, blocks, 0);
+        k_fq12_reduce_wide<<<dim3((unsigned)blocks, sets), kBlock, 0, s>>>(src, sstride, sn, sset, dst,
+                                                                            sets * blocks, 0, blocks);
         HIPCHK(c, hipGetLastError());
         src = dst;
-        sstride = blocks;
+        sstride = sets * blocks;
         sn = blocks;
+        sset = blocks;
         a = !a;
     }
 }
@@ -294,7 +299,7 @@ int run_fe(bn_ctx* c, const uint32_t* f, size_t n, const uint8_t* flags, bn_gt* 
 }
 
 // ---- pairing_batch / miller_loop_batch: segmented Miller loop + device reduction
-constexpr int kRegionSeg = 8;  // k_miller_seg output: segment g in region kRegionSeg + g
+constexpr int kRegionSeg = 8;  // k_miller_seg output: S * n elements from region kRegionSeg on
 
 // S segments of the 64 NAF digits (S doubles until S * n pairs fill about
 // 2^16 lane pairs, i.e. two waves per SIMD), cut so each carries about the same
@@ -333,12 +338,10 @@ int chunk_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int m
     k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags, c->d_err, mode);
     HIPCHK(c, hipGetLastError());
     k_miller_seg<<<grid_for(kPathLanes * plan.S * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
-                                                                       slot_region(c, kRegionSeg),
-                                                                       (size_t)kSlotWords * c->cap);
+                                                                       slot_region(c, kRegionSeg));
     HIPCHK(c, hipGetLastError());
-    for (int g = 0; g < plan.S; ++g)
-        RET_IF(product_wide(c, slot_region(c, kRegionSeg + g), m, m, parts, plan.S * nchunks, g * nchunks + k, s));
-    return BN_OK;
+    return product_wide(c, slot_region(c, kRegionSeg), plan.S * m, m, m, plan.S, parts, plan.S * nchunks, k, nchunks,
+                        s);
 }
 // where chunk partials go: straight into the result region (element g, stride S)
 // for one chunk, else the parts region
@@ -348,13 +351,10 @@ uint32_t* parts_region(bn_ctx* c, size_t nchunks) {
 // per segment, the chunk partials -> the result region; then the Horner
 // recombination (+ the final exponentiation for pairing_batch) into *d_out
 int finish_product(bn_ctx* c, const SegPlan& plan, size_t nchunks, int do_fe, bn_gt* d_out, hipStream_t s) {
-    if (nchunks > 1) {
-        uint32_t* parts = slot_region(c, kRegionParts);
-        for (int g = 0; g < plan.S; ++g)
-            RET_IF(product_wide(c, parts + 2 * g * nchunks, plan.S * nchunks, nchunks, slot_region(c, kRegionResult),
-                                plan.S, g, s));
-    }
-    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err);
+    if (nchunks > 1)
+        RET_IF(product_wide(c, slot_region(c, kRegionParts), plan.S * nchunks, nchunks, nchunks, plan.S,
+                            slot_region(c, kRegionResult), plan.S, 0, 1, s));
+    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, plan, do_fe, d_out, c->d_err);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
@@ -475,6 +475,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
     c->device = device;
     c->fe_wide_max = kFeWideMaxDefault;
     if (const char* e = getenv("BN254MI_FE_WIDE_MAX")) c->fe_wide_max = (size_t)strtoull(e, nullptr, 10);
+    if (const char* e = getenv("BN254MI_MILLER_FORM")) c->miller_form = atoi(e);
     Prog P;
     c->fe_out = (int)build_final_exp(P);
     P.finalize({(uint32_t)c->fe_out});
@@ -555,9 +556,40 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             if (c->timing && ev[k]) hipEventRecord(ev[k], s);
         };
         mark(0);
-        k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags, c->d_err, 0);
-        mark(1);
-        k_miller<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, c->slots);
+        if (m <= c->fe_wide_max) {
+            // latency path: the Miller loop in segments on 2 * S lanes per pairing,
+            // recombined and exponentiated on a 16-lane group per pairing
+            const SegPlan plan = seg_plan(m);
+            k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags,
+                                                                  c->d_err, 0);
+            mark(1);
+            k_miller_seg<<<grid_for(kPathLanes * plan.S * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
+                                                                               slot_region(c, kRegionSeg));
+            mark(2);
+            k_horner_wide<<<grid_for(16 * m), kBlock, 0, s>>>(slot_region(c, kRegionSeg), m, plan, 1, d_out + off,
+                                                              c->d_err);
+            mark(3);
+            mark(4);
+            HIPCHK(c, hipGetLastError());
+            if (c->timing) c->ev_marks.push_back(ev);
+            continue;
+        }
+        if (c->miller_form == 1) {
+            k_pairing_fused<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->flags, c->d_err, 0,
+                                                                        c->slots);
+            mark(1);
+        } else {
+            k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags,
+                                                                  c->d_err, 0);
+            mark(1);
+            if (c->miller_form == 2) {  // the segment kernel with one segment: the whole loop
+                const SegPlan whole = seg_plan(~(size_t)0 >> 1);
+                k_miller_seg<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, whole,
+                                                                          c->slots);
+            } else {
+                k_miller<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, c->slots);
+            }
+        }
         mark(2);
         if (m <= c->fe_wide_max) {  // latency: 16 lanes per element (kernels_wide.hip)
             k_fe_wide<<<grid_for(16 * m), kBlock, 0, s>>>(c->slots, m, m, d_out + off, nullptr, c->d_err);

@@ -30,6 +30,12 @@ struct bn_ctx {
     // wide layout (kernels_wide.hip, 16 lanes per element: latency) instead of
     // the step machine (k_fq12_vm, 2 lanes per element: throughput)
     size_t fe_wide_max = 0;
+    // A/B switch ($BN254MI_MILLER_FORM) for bn_pairing_many_dev batches above the
+    // wide threshold: 1 (default, measured fastest) = to_affine,
+    // line steps and Miller loop fused in one kernel (k_pairing_fused, no
+    // coefficient traffic); 0 = k_prepare (line coefficients to HBM) + k_miller;
+    // 2 = k_prepare + k_miller_seg with one segment
+    int miller_form = 1;
     int* d_err = nullptr;
     // staging for host-buffer calls (device)
     size_t stage_bytes = 0;

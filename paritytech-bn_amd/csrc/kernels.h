@@ -425,27 +425,30 @@ struct SegPlan {
 __global__ void __launch_bounds__(kBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
                                                        const uint32_t* __restrict__ paff,
                                                        const uint8_t* __restrict__ flags, size_t n, SegPlan plan,
-                                                       uint32_t* __restrict__ out, size_t seg_words);
-// out = Horner recombination of the S segment values g[s] (element s, stride S, split
-// layout): x = g0; x = x^(2^len_s) * g_s; then the final exponentiation when do_fe
-__global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, SegPlan plan, int do_fe,
-                                                        bn_gt* __restrict__ out, int* __restrict__ err);
+                                                       uint32_t* __restrict__ out);
+// out[e] = Horner recombination of element e's S segment values (element s * n + e of g,
+// split layout, stride S * n): x = g0; x = x^(2^len_s) * g_s; then the final
+// exponentiation when do_fe
+__global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, size_t n, SegPlan plan,
+                                                        int do_fe, bn_gt* __restrict__ out, int* __restrict__ err);
 __global__ void __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
                           uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
                           int* __restrict__ err, int mode);
+__global__ void __launch_bounds__(kBlock) k_pairing_fused(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
+                                                          size_t n, uint8_t* __restrict__ flags, int* __restrict__ err,
+                                                          int mode, uint32_t* __restrict__ f_out);
 __global__ void __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ coeffs, const uint32_t* __restrict__ paff,
                          const uint8_t* __restrict__ flags, size_t n, uint32_t* __restrict__ f_out);
 __global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps, uint32_t* slots, size_t n);
 __global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot, const uint8_t* __restrict__ flags,
                          bn_gt* __restrict__ out, uint8_t* __restrict__ ok, int* __restrict__ err);
-__global__ void __launch_bounds__(kBlock) k_fq12_product(uint32_t* __restrict__ f, size_t stride, size_t m, size_t half);
 // kernels_wide.hip (fq12_wide.h): final exponentiation and product reduction on 16-lane groups
 __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__ f, size_t stride, size_t n,
                                                     bn_gt* __restrict__ out, uint8_t* __restrict__ ok,
                                                     int* __restrict__ err);
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
-                                                             size_t n, uint32_t* __restrict__ out,
-                                                             size_t out_stride, size_t out_base);
+                                                             size_t n, size_t in_set, uint32_t* __restrict__ out,
+                                                             size_t out_stride, size_t out_base, size_t out_set);
 __global__ void __launch_bounds__(kBlock) k_err_status(const int* __restrict__ err, int* __restrict__ status);
 __global__ void __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g, size_t n, uint32_t* __restrict__ f);
 __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict__ f, size_t n, size_t stride, bn_gt* __restrict__ g);

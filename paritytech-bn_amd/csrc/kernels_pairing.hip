@@ -16,17 +16,18 @@ namespace bn {
 constexpr size_t kL = BN_SPLIT ? 2 : 1;  // lanes per pairing in this translation unit
 
 // ---------------------------------------------------------------- pairing kernels
-// flags[lane]: 1 = skip (a zero point; pairing() returns Fq12::one(), mod.rs:896)
-// mode 1 (miller_loop_batch): a zero point sets *err = BN_ERR_TO_AFFINE (lib.rs:629-630)
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
-                                                                size_t n, uint32_t* __restrict__ coeffs,
-                                                                uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
-                                                                int* __restrict__ err, int mode) {
-    fold_table_init();
-    const size_t l = lane_id(), i = l / kL, nl = kL * n;
-    if (i >= n) return;
+// to_affine of both points of pair i (mod.rs:199-216; the z == 1 shortcut yields
+// the same values as the general path).  flags[lane]: 1 = skip (a zero point;
+// pairing() returns Fq12::one(), mod.rs:896); mode 1 (miller_loop_batch): a zero
+// point sets *err = BN_ERR_TO_AFFINE (lib.rs:629-630).
+struct PairAffine {
+    Fq<2> px, py;
+    G2Aff<kPt> qa;
+};
+__device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t i,
+                                                     size_t l, uint8_t* __restrict__ flags, int* __restrict__ err,
+                                                     int mode) {
     uint32_t w[8];
-    // to_affine (mod.rs:199-216); the z == 1 shortcut yields the same values as the general path
     ld_words(&p[i].z, w);
     const bool p_zero = words_zero(w);
     const Fq<2> pz = fq_load_ref(w);
@@ -58,11 +59,9 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare(const bn_g1* __
     const auto pzinv = fq_mul(t, nq);
     const auto ninv = fq_mul(t, pz);
     auto pzinv2 = fq_sqr(pzinv);
-    auto px = fq_mul(ld_ref(p[i].x), pzinv2);
-    auto py = fq_mul(ld_ref(p[i].y), fq_mul(pzinv2, pzinv));
-    st_fq(paff, nl, l, 0, px);
-    st_fq(paff, nl, l, 1, py);
-
+    PairAffine a;
+    a.px = fq_mul(ld_ref(p[i].x), pzinv2);
+    a.py = fq_mul(ld_ref(p[i].y), fq_mul(pzinv2, pzinv));
 #if BN_SPLIT
     const auto zn = fq_mul(qz.c, ninv);
     const auto qzinv = wrap2(fq_select(lane_odd(), fq_neg(zn), zn));  // conj(qz) * ninv
@@ -70,13 +69,44 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare(const bn_g1* __
     const auto qzinv = mk2(fq_mul(qz.c0, ninv), fq_neg(fq_mul(qz.c1, ninv)));
 #endif
     auto qzinv2 = fq2_sqr(qzinv);
-    G2Aff<kPt> qa = {narrow<kPt>(fq2_mul(ld_ref2(q[i].x), qzinv2)),
-                     narrow<kPt>(fq2_mul(ld_ref2(q[i].y), fq2_mul(qzinv2, qzinv)))};
-    g2_precompute(qa, [&](int k, const Ell& e) {
+    a.qa = {narrow<kPt>(fq2_mul(ld_ref2(q[i].x), qzinv2)), narrow<kPt>(fq2_mul(ld_ref2(q[i].y), fq2_mul(qzinv2, qzinv)))};
+    return a;
+}
+
+// to_affine + the 87 line coefficients (AffineG2::precompute) -> HBM
+__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
+                                                                size_t n, uint32_t* __restrict__ coeffs,
+                                                                uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
+                                                                int* __restrict__ err, int mode) {
+    fold_table_init();
+    const size_t l = lane_id(), i = l / kL, nl = kL * n;
+    if (i >= n) return;
+    const PairAffine a = pair_to_affine(p, q, i, l, flags, err, mode);
+    st_fq(paff, nl, l, 0, a.px);
+    st_fq(paff, nl, l, 1, a.py);
+    g2_precompute(a.qa, [&](int k, const Ell& e) {
         st_fq2(coeffs, nl, l, k * 6 + 0, e.ell_0);
         st_fq2(coeffs, nl, l, k * 6 + 2, e.ell_vw);
         st_fq2(coeffs, nl, l, k * 6 + 4, e.ell_vv);
     });
+}
+
+// A/B form ("line coefficients"): to_affine, the line steps and the
+// Miller loop fused in one kernel -- each coefficient is applied as soon as it is
+// computed and never leaves registers (no 16.7 KB/pairing HBM round trip).  Same
+// operations in the same order as k_prepare + k_miller, so the same Miller value.
+__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_pairing_fused(const bn_g1* __restrict__ p,
+                                                                      const bn_g2* __restrict__ q, size_t n,
+                                                                      uint8_t* __restrict__ flags,
+                                                                      int* __restrict__ err, int mode,
+                                                                      uint32_t* __restrict__ f_out) {
+    fold_table_init();
+    const size_t l = lane_id(), i = l / kL, nl = kL * n;
+    if (i >= n) return;
+    const PairAffine a = pair_to_affine(p, q, i, l, flags, err, mode);
+    Fq12<kF> f = miller_fused(a.qa, a.px, a.py);
+    if (flags[l]) f = widen<kF>(fq12_one());
+    st_fq12(f_out, nl, l, f);
 }
 
 __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ coeffs,
@@ -99,13 +129,12 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* 
 // Miller loop in segments (pairing_batch / miller_loop_batch with fewer pairs
 // than fill the GPU): lane pair (segment s, pair i) -- segment-major, so a wave
 // reads consecutive pairs' coefficients -- computes pair i's loop over the
-// segment's digits (pairing.h miller_segment) into element i of
-// out + s * seg_words.  Segment values of a pair with a zero point are one.
+// segment's digits (pairing.h miller_segment) into element s * n + i of `out`
+// (split layout, stride S * n).  Segment values of a pair with a zero point are one.
 __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
                                                                    const uint32_t* __restrict__ paff,
                                                                    const uint8_t* __restrict__ flags, size_t n,
-                                                                   SegPlan plan, uint32_t* __restrict__ out,
-                                                                   size_t seg_words) {
+                                                                   SegPlan plan, uint32_t* __restrict__ out) {
     fold_table_init();
     const size_t l = lane_id(), pr = l / kL, nl = kL * n;
     if (pr >= (size_t)plan.S * n) return;
@@ -118,7 +147,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller_seg(const uint32
                    ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 4)};
     });
     if (flags[lt]) f = widen<kF>(fq12_one());
-    st_fq12(out + (size_t)s * seg_words, nl, lt, f);
+    st_fq12(out, kL * plan.S * n, l, f);
 }
 
 }  // namespace bn

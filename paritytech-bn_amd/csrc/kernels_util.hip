@@ -1,4 +1,4 @@
-// kernels_util.hip -- product tree over Miller values and Gt image <-> lane-strided conversion.
+// kernels_util.hip -- Gt image <-> lane-strided conversion.
 // Pairing-path layout (BN_PATH_SPLIT: two lanes per element, kernels.h); n,
 // m, half and stride count elements, the grid has kPathLanes threads each.
 #include "fq.h"
@@ -8,17 +8,6 @@
 namespace bn {
 
 constexpr size_t kL = BN_SPLIT ? 2 : 1;  // lanes per element in this translation unit
-
-// f[e] *= f[e + half] for e + half < m: one level of the product tree (slot stride `stride` elements)
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_fq12_product(uint32_t* __restrict__ f, size_t stride, size_t m,
-                                                                     size_t half) {
-    fold_table_init();
-    const size_t l = lane_id(), e = l / kL;
-    if (e >= half || e + half >= m) return;
-    Fq12<kF> a = ld_fq12_buf<kF>(f, kL * stride, l);
-    Fq12<kF> b = ld_fq12_buf<kF>(f, kL * stride, l + kL * half);
-    st_fq12_buf(f, kL * stride, l, mul12(a, b));
-}
 
 // Gt images <-> lane-strided internal Fq12
 __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g, size_t n,

@@ -45,26 +45,27 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
     if (w.l < 12) st_words(&out[e].c[w_gt_index(w)], words);
 }
 
-// Product reduction: block b multiplies elements [32b, 32b + 32) of `in` (split
-// layout, `n` elements, stride in_stride) -- one product per group of the two
-// elements 2g, 2g + 1, then a tree over the 16 groups through LDS -- and writes
-// the block's product as element out_base + b of `out` (stride out_stride).  Elements past
-// n count as one.  The order of the factors differs from the reference's
-// left-to-right accumulation; Fq12 multiplication is commutative and
-// associative, so the value is the same.
+// Product reduction of several independent sets (blockIdx.y = set y, the
+// elements y * in_set + [0, n) of `in`, split layout, stride in_stride): block
+// (b, y) multiplies the set's elements [32b, 32b + 32) -- one product per group
+// of the two elements 2g, 2g + 1, then a tree over the 16 groups through LDS --
+// and writes the block's product as element out_base + y * out_set + b of `out`
+// (stride out_stride).  Elements past n count as one.  The order of the factors
+// differs from the reference's left-to-right accumulation; Fq12 multiplication
+// is commutative and associative, so the value is the same.
 __shared__ uint32_t g_wval[kWGroups * kWLanes * kWSlot];  // 12 KB: one value per group
 
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
-                                                             size_t n, uint32_t* __restrict__ out,
-                                                             size_t out_stride, size_t out_base) {
+                                                             size_t n, size_t in_set, uint32_t* __restrict__ out,
+                                                             size_t out_stride, size_t out_base, size_t out_set) {
     fold_table_init();
     const WL w = wl();
     const int g = (int)threadIdx.x / kWLanes;
     const size_t base = (size_t)blockIdx.x * 2 * kWGroups;
-    const size_t e0 = base + 2 * g, e1 = e0 + 1;
+    const size_t e0 = base + 2 * g, e1 = e0 + 1, sb = (size_t)blockIdx.y * in_set;
     const Fq<2> one = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
-    const Fq<2> a = e0 < n ? w_ld_split(in, in_stride, e0, w) : one;
-    const Fq<2> b = e1 < n ? w_ld_split(in, in_stride, e1, w) : one;
+    const Fq<2> a = e0 < n ? w_ld_split(in, in_stride, sb + e0, w) : one;
+    const Fq<2> b = e1 < n ? w_ld_split(in, in_stride, sb + e1, w) : one;
     Fq<2> x = e1 < n ? w12_mul(a, b) : a;  // uniform per group
     uint32_t* mine = g_wval + (g * kWLanes) * kWSlot;
 #pragma unroll 1
@@ -77,25 +78,29 @@ __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __r
         }
         __syncthreads();
     }
-    if (g == 0) w_st_split(out, out_stride, out_base + blockIdx.x, w, x);
+    if (g == 0) w_st_split(out, out_stride, out_base + blockIdx.y * out_set + blockIdx.x, w, x);
 }
 
-// Recombination of a segmented Miller loop (pairing.h miller_segment): x = g_0,
-// then x = x^(2^len_s) * g_s for s = 1..S-1 (the generic squaring, as the
-// reference's loop squares its accumulator), then pairing_batch's final
-// exponentiation when do_fe (zero -> zero image + error bit) or the Miller
-// value itself (miller_loop_batch).  One 16-lane group.
-__global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, SegPlan plan, int do_fe,
-                                                        bn_gt* __restrict__ out, int* __restrict__ err) {
+// Recombination of segmented Miller loops (pairing.h miller_segment), one
+// 16-lane group per element e < n: segment s of element e is element s * n + e
+// of g (split layout, stride S * n, as k_miller_seg writes it).  x = g_0, then
+// x = x^(2^len_s) * g_s for s = 1..S-1 (the generic squaring, as the reference's
+// loop squares its accumulator), then the final exponentiation when do_fe
+// (pairing / pairing_batch; zero -> zero image + error bit) or the Miller value
+// itself (miller_loop_batch) -> out[e].
+__global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, size_t n, SegPlan plan,
+                                                        int do_fe, bn_gt* __restrict__ out, int* __restrict__ err) {
     fold_table_init();
-    if (w_elem() >= 1) return;
+    const size_t e = w_elem();
+    if (e >= n) return;
     const WL w = wl();
-    Fq<2> x = w_ld_split(g, plan.S, 0, w);
+    const size_t stride = (size_t)plan.S * n;
+    Fq<2> x = w_ld_split(g, stride, e, w);
 #pragma unroll 1
     for (int s = 1; s < plan.S; ++s) {
 #pragma unroll 1
         for (int k = plan.lo[s]; k < plan.hi[s]; ++k) x = w12_mul(x, x);
-        x = w12_mul(x, w_ld_split(g, plan.S, s, w));
+        x = w12_mul(x, w_ld_split(g, stride, (size_t)s * n + e, w));
     }
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (do_fe) {
@@ -106,7 +111,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
     } else {
         fq_store_ref(x, words);
     }
-    if (w.l < 12) st_words(&out->c[w_gt_index(w)], words);
+    if (w.l < 12) st_words(&out[e].c[w_gt_index(w)], words);
 }
 
 // *status = the bn_status of the device-side outcome bits in *err (bn_*_batch_dev)

@@ -63,6 +63,31 @@ BN_INLINE Fq12<kF> miller_loop(const Fq<PB>& px, const Fq<PB>& py, Line&& line) 
     return f;
 }
 
+// The Miller loop with the line steps inline (k_pairing_fused): the
+// coefficients of g2_precompute applied as they are produced, in
+// G2Precomp::miller_loop's order (mod.rs:579-607, 701-727)
+template <int B, int PB>
+BN_INLINE Fq12<kF> miller_fused(const G2Aff<B>& q, const Fq<PB>& px, const Fq<PB>& py) {
+    G2Proj r = {widen<kPt>(q.x), widen<kPt>(q.y), widen<kPt>(fq2_one())};
+    const G2Aff<B> q_neg = {q.x, fq2_neg(q.y)};
+    Fq12<kF> f = widen<kF>(fq12_one());
+#pragma unroll 1
+    for (int i = 0; i < BN_NAF_DIGITS; ++i) {
+        f = apply_line(narrow12<kF>(fq12_sqr(f)), doubling_step(r), px, py);
+        if ((kNafNonzero >> i) & 1u) {
+            const bool minus = (kNafMinus >> i) & 1u;
+            G2Aff<B> base = {q.x, fq2_select(minus, q_neg.y, q.y)};
+            f = apply_line(f, mixed_addition_step(r, base), px, py);
+        }
+    }
+    G2Aff<kPt> q1 = mul_by_q(q);
+    G2Aff<kPt> q2 = mul_by_q(q1);
+    q2.y = fq2_neg(q2.y);
+    f = apply_line(f, mixed_addition_step(r, q1), px, py);
+    f = apply_line(f, mixed_addition_step(r, q2), px, py);
+    return f;
+}
+
 // One segment of the Miller loop: digits [lo, hi) starting from f = one, with
 // line coefficients from index `idx` on; the last segment (hi == 64) also
 // applies the two lines after the loop.  Running the loop over digits
