@@ -192,10 +192,13 @@ int bn_gt_pow_many_dev(bn_ctx* ctx, const bn_gt* d_a, const bn_fr* d_k, size_t n
 /* enable HIP-event timing of each kernel phase of bn_pairing_many_dev (events are
  * recorded on the launch stream between the kernels) */
 int bn_set_phase_timing(bn_ctx* ctx, int enable);
-/* Batches of at most n elements run the final exponentiation on 16-lane groups
- * (latency path, kernels_wide.hip); larger ones on the two-lane step machine
- * (throughput path, k_fq12_vm).  Default 4096 or $BN254MI_FE_WIDE_MAX; results are
- * identical either way.  On a multi-device context it applies to every device. */
+/* Batches of at most n elements take the latency path: bn_pairing_many_dev runs the
+ * Miller loop in segments and the recombination + final exponentiation on 16-lane
+ * groups, bn_final_exponentiation_many the 16-lane final exponentiation
+ * (kernels_wide.hip); larger batches take the throughput path (k_pairing_fused +
+ * the two-lane step machine k_fq12_vm).  Default 8192 (the measured crossover) or
+ * $BN254MI_FE_WIDE_MAX; results are identical either way.  On a multi-device
+ * context it applies to every device. */
 int bn_set_fe_wide_max(bn_ctx* ctx, size_t n);
 /* device milliseconds per phase since the last read: ms[0] k_prepare (to_affine +
  * G2 lines), ms[1] k_miller, ms[2] final exponentiation (k_fq12_vm, or k_fe_wide for

@@ -57,9 +57,11 @@ int ws_drain(bn_ctx* c) {
 }
 
 constexpr int kFeSlots = 32;  // slot 0: Miller value, 1: easy-part result, 2..: temporaries
-// batches up to this size run the final exponentiation on the wide layout
-// (measured crossover; BN254MI_FE_WIDE_MAX or bn_set_fe_wide_max override)
-constexpr size_t kFeWideMaxDefault = 4096;
+// batches up to this size take the latency path (segmented Miller loop, Horner
+// + final exponentiation on 16-lane groups); measured crossover with the
+// throughput path: 8192 pairs 3.58 vs 5.43 ms, 16384 pairs 6.05 vs 5.43 ms
+// (profiles/r2j_latency_sweep.jsonl).  BN254MI_FE_WIDE_MAX or bn_set_fe_wide_max override.
+constexpr size_t kFeWideMaxDefault = 8192;
 
 size_t ws_bytes(size_t n) {
     return n * ((size_t)kCoeffFq * 9 * 4 + kPathLanes * (2 * 9 * 4 + 1) + (size_t)kFeSlots * kSlotWords * 4) + 64;

@@ -42,7 +42,7 @@ def test_final_exp_both_layouts(ctx, pairs):
         ctx.set_fe_wide_max(0)
         vm, ok_v = ctx.final_exponentiation_many(f)
     finally:
-        ctx.set_fe_wide_max(4096)
+        ctx.set_fe_wide_max(8192)
     assert np.array_equal(wide, vm) and np.array_equal(ok_w, ok_v)
     assert list(ok_w) == [1] * 40 + [0, 1]
     assert np.array_equal(wide, want)

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--sizes", default="1,2,4,8,16,64,256,1024,4096")
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--calls", default="pairing_many,pairing_batch,pairing_many_dev")
+    ap.add_argument("--fe-wide-max", type=int, default=None,
+                    help="batches up to this size take the latency path (bn_set_fe_wide_max)")
     args = ap.parse_args()
     import torch
 
@@ -44,6 +46,8 @@ def main():
 
     dev = torch.device("cuda", 0)
     ctx = Context(0)
+    if args.fe_wide_max is not None:
+        ctx.set_fe_wide_max(args.fe_wide_max)
     sizes = [int(s) for s in args.sizes.split(",")]
     nmax = max(sizes)
     s, t = synth.dataset_scalars(0, nmax)
@@ -82,7 +86,7 @@ def main():
             fn()
             dt = med(fn, args.reps)
             print(json.dumps({"call": call, "n": n, "ms": dt * 1e3, "per_item_us": dt / n * 1e6,
-                              "cpu_1thread_ms": cpu1 * n * 1e3}), flush=True)
+                              "cpu_1thread_ms": cpu1 * n * 1e3, "fe_wide_max": args.fe_wide_max}), flush=True)
 
 
 if __name__ == "__main__":
