@@ -118,6 +118,11 @@ int bn_final_exponentiation_many(bn_ctx* ctx, const bn_gt* f, size_t n, bn_gt* o
  * precompute; a pair with a zero point gives Fq12::one() */
 int bn_miller_loop_many(bn_ctx* ctx, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out);
 
+/* the line coefficients of AffineG2::precompute (mod.rs:701-727) of q[i] after
+ * to_affine: out[(i * 87 + k) * 3 + j] = coefficient k's (ell_0, ell_vw, ell_vv)[j]
+ * (G2Precomp / EllCoeffs, mod.rs:566-577).  BN_ERR_TO_AFFINE if a q is zero. */
+int bn_g2_precompute_many(bn_ctx* ctx, const bn_g2* q, size_t n, bn_fq2* out);
+
 /* ---- group path (src/groups/mod.rs:250-334, lib.rs:425-431) ---- */
 
 /* out[i] = p[i] * k[i]: the reference's double-and-add chain (mod.rs:272-292), so the

@@ -833,6 +833,40 @@ int bn_miller_loop_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_
     return BN_OK;
 }
 
+int bn_g2_precompute_many(bn_ctx* c, const bn_g2* q, size_t n, bn_fq2* out) {
+    CTX_GUARD_HOST(c);
+    if (n == 0) return BN_OK;
+    if (!q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    RET_IF(clear_err(c, c->stream));
+    bn_g1 one;  // k_prepare converts a G1 point too; G1::one() (z = 1) is never zero
+    memset(&one, 0, sizeof one);
+    one.x.l[0] = 0xd35d438dc58f0d9dull, one.x.l[1] = 0x0a78eb28f5c70b3dull;  // Fq::one(): R mod p
+    one.x.l[2] = 0x666ea36f7879462cull, one.x.l[3] = 0x0e0a77c19a07df2full;
+    one.z = one.x;
+    for (size_t off = 0; off < n; off += kChunk) {
+        const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
+        RET_IF(reserve(c, m));
+        const size_t out_bytes = m * (size_t)BN_NUM_COEFFS * 3 * sizeof(bn_fq2);
+        RET_IF(stage(c, m * (sizeof(bn_g1) + sizeof(bn_g2)) + out_bytes));
+        bn_g1* dp = (bn_g1*)c->stage;
+        bn_g2* dq = (bn_g2*)(dp + m);
+        bn_fq2* dout = (bn_fq2*)(dq + m);
+        std::vector<bn_g1> ones(m, one);
+        HIPCHK(c, hipMemcpyAsync(dp, ones.data(), m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
+        k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(dp, dq, m, c->coeffs, c->paff, c->flags,
+                                                                       c->d_err, 1);
+        k_coeffs_store<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(c->coeffs, m, dout);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(out + off * BN_NUM_COEFFS * 3, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    int bits = 0;
+    RET_IF(check_err(c, c->stream, &bits));
+    if (bits & (1 << BN_ERR_TO_AFFINE)) return fail(c, BN_ERR_TO_AFFINE, "ToAffineConversion");
+    return BN_OK;
+}
+
 int bn_g1_mul_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_fr* d_k, size_t n, bn_g1* d_out, void* stream) {
     CTX_GUARD(c);
     if (n == 0) return BN_OK;

@@ -91,6 +91,19 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare(const bn_g1* __
     });
 }
 
+// The coefficients k_prepare wrote for pair i -> the reference images of its
+// G2Precomp (mod.rs:566-577): 87 x {ell_0, ell_vw, ell_vv}, each a canonical Fq2
+__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_coeffs_store(const uint32_t* __restrict__ coeffs, size_t n,
+                                                                     bn_fq2* __restrict__ out) {
+    fold_table_init();
+    const size_t l = lane_id(), i = l / kL, nl = kL * n;
+    if (i >= n) return;
+#pragma unroll 1
+    for (int k = 0; k < BN_NUM_COEFFS; ++k)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) st_ref2(out[(i * BN_NUM_COEFFS + k) * 3 + j], ld_fq2<kLine>(coeffs, nl, l, k * 6 + 2 * j));
+}
+
 // A/B form ("line coefficients"): to_affine, the line steps and the
 // Miller loop fused in one kernel -- each coefficient is applied as soon as it is
 // computed and never leaves registers (no 16.7 KB/pairing HBM round trip).  Same

@@ -34,7 +34,7 @@ EXPORTS = [
     "bn_g2_affine_new_many", "bn_g2_affine_new_many_dev", "bn_g1_from_compressed_many", "bn_g2_from_compressed_many",
     "bn_g1_from_compressed_many_dev", "bn_g2_from_compressed_many_dev", "bn_gt_pow_many", "bn_gt_pow_many_dev",
     "bn_ctx_create_multi", "bn_ctx_num_devices", "bn_ctx_device", "bn_shard_range", "bn_pairing_many_allgather_dev",
-    "bn_pairing_batch_dev", "bn_miller_loop_batch_dev", "bn_set_fe_wide_max",
+    "bn_pairing_batch_dev", "bn_miller_loop_batch_dev", "bn_set_fe_wide_max", "bn_g2_precompute_many",
 ]
 
 # per-element status (bn_elem_status)
@@ -113,6 +113,7 @@ def load():
         "bn_pairing_batch_dev": ([vp, vp, vp, sz, vp, vp, vp], i),
         "bn_miller_loop_batch_dev": ([vp, vp, vp, sz, vp, vp, vp], i),
         "bn_set_fe_wide_max": ([vp, sz], i),
+        "bn_g2_precompute_many": ([vp, vp, sz, vp], i),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -230,6 +231,14 @@ class Context:
         _same_rows(p, q)
         out = np.zeros((p.shape[0], 48), np.uint64)
         self._check(self._L.bn_miller_loop_many(self._h, _ptr(p), _ptr(q), p.shape[0], _ptr(out)))
+        return out
+
+    def g2_precompute_many(self, q):
+        """AffineG2::precompute of each (Jacobian) q: (n, 87, 24) uint64 -- per coefficient
+        ell_0, ell_vw, ell_vv (mod.rs:566-577, 701-727)."""
+        q = _arr(q, 24)
+        out = np.zeros((q.shape[0], 87, 24), np.uint64)
+        self._check(self._L.bn_g2_precompute_many(self._h, _ptr(q), q.shape[0], _ptr(out)))
         return out
 
     def final_exponentiation_many(self, f):

@@ -183,3 +183,36 @@ def test_large_batch_parity_and_bilinearity(ctx):
     # spot-check a sample of lanes against the oracle
     idx = np.random.default_rng(0).choice(n, 256, replace=False)
     assert np.array_equal(e1[idx], O.pairing_many(sP[idx], Q[idx], NT))
+
+
+def test_prepared_g2_on_gpu(ctx, kats, pairs):
+    """All 87 line coefficients computed on the GPU (bn_g2_precompute_many):
+    the reference's test_prepared_g2 vector (src/groups/mod.rs:780-892) and 64
+    random points against the oracle's G2Precomp, bit for bit; a zero point is
+    ToAffineConversion."""
+    from substrate_bn import BnError
+    t = kats["test_prepared_g2"]
+    q = O.g2_mul(O.g2_one(), O.canon_to_mont_array([int(t["g2_scalar"])], O.FR))
+    c = ctx.g2_precompute_many(q)
+    assert c.shape == (1, 87, 24)
+    assert O.mont_array_to_canon(c.reshape(-1)) == [int(x) for row in t["coeffs"] for x in row]
+    _, qs = pairs
+    got = ctx.g2_precompute_many(qs[:64])
+    for k in range(64):
+        qa, rc = O.g2_to_affine(qs[k])
+        assert rc == [0] and np.array_equal(got[k], O.g2_precompute(qa[0])), k
+    z = qs[:2].copy()
+    z[1] = 0
+    z[1, 8:12] = O.canon_to_mont_array([1])   # G2::zero()
+    with pytest.raises(BnError):
+        ctx.g2_precompute_many(z)
+
+
+def test_config3_g1_mul_full_size(ctx):
+    """BASELINE config 3 at its full size: 2^18 G1 * Fr on random Jacobian bases and
+    uniform scalars, every lane bit-exact (raw Jacobian image) against the oracle."""
+    n = 1 << 18
+    _, S = O.random_scalars(n, seed=333, lo=0)
+    base = ctx.g1_mul_many(np.tile(O.g1_one(), (n, 1)), np.roll(S, 7, axis=0))  # random Jacobian bases (z != 1)
+    got = ctx.g1_mul_many(base, S)
+    assert np.array_equal(got, O.g1_mul(base, S, NT))
