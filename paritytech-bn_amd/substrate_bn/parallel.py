@@ -49,6 +49,42 @@ def pairing_many_distributed(p, q, compute=None, device=None):
                            for r in range(world)], axis=0)
 
 
+def pairing_many_distributed_dev(P, Q, compute=None, stream=None):
+    """Device-resident form (BASELINE config 4 as a library call): P (n, 12) and
+    Q (n, 24) int64 tensors holding the reference images, the same on every rank
+    (or at least this rank's shard); each rank pairs its contiguous shard into a
+    buffer on its own device and one all_gather_into_tensor (RCCL over xGMI with
+    the nccl backend) returns all n results, (n, 48) int64, on every rank -- no
+    host round trip.  `compute(P_shard, Q_shard, out)` fills `out`; by default
+    the engine's bn_pairing_many_dev on `stream` (a torch.cuda.Stream, or the
+    context's own stream), and torch's current stream -- where the collective
+    is issued -- waits for it."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    n = P.shape[0]
+    lo, hi = shard_bounds(n, rank, world)
+    max_rows = max(shard_bounds(n, r, world)[1] - shard_bounds(n, r, world)[0] for r in range(world))
+    buf = torch.zeros((max_rows, 48), dtype=torch.int64, device=P.device)
+    engine_stream = None
+    if compute is None:
+        from . import context
+        ctx = context()
+        engine_stream = stream if stream is not None else torch.cuda.ExternalStream(ctx.stream, device=P.device)
+        engine_stream.wait_stream(torch.cuda.current_stream(P.device))  # inputs and buf are ready
+
+        def compute(a, b, out):
+            ctx.pairing_many_dev(a.data_ptr(), b.data_ptr(), a.shape[0], out.data_ptr(), engine_stream.cuda_stream)
+    if hi > lo:
+        compute(P[lo:hi].contiguous(), Q[lo:hi].contiguous(), buf[:hi - lo])
+    if engine_stream is not None:
+        torch.cuda.current_stream(P.device).wait_stream(engine_stream)
+    gathered = torch.empty((world * max_rows, 48), dtype=torch.int64, device=P.device)
+    dist.all_gather_into_tensor(gathered, buf)
+    if max_rows * world == n:
+        return gathered
+    return torch.cat([gathered[r * max_rows:r * max_rows + shard_bounds(n, r, world)[1]
+                               - shard_bounds(n, r, world)[0]] for r in range(world)])
+
+
 def pairing_batch_distributed(p, q, miller_product=None, fq12_mul=None, final_exp=None, device=None):
     """pairing_batch over the whole batch (mod.rs:904-926), identical Gt on every rank."""
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -61,8 +97,9 @@ def pairing_batch_distributed(p, q, miller_product=None, fq12_mul=None, final_ex
         fq12_mul = lambda a, b: ctx.fq12_op_many("mul", a, b)[0]  # noqa: E731
         final_exp = lambda f: ctx.final_exponentiation_many(f)  # noqa: E731
     # zero points are skipped (mod.rs:911-920): drop them before the product
+    # (zero iff z == 0: G1 z is words 8..11, G2 z words 16..23)
     ps, qs = p[lo:hi], q[lo:hi]
-    keep = np.array([bool(a[8:12].any()) and bool(b[16:24].any()) for a, b in zip(ps, qs)], dtype=bool)
+    keep = ps[:, 8:12].any(axis=1) & qs[:, 16:24].any(axis=1)
     ps, qs = ps[keep], qs[keep]
     local = miller_product(ps, qs) if ps.shape[0] else None
     flag = np.zeros((1, 48), np.uint64)

@@ -35,6 +35,14 @@ def worker(rank, world, port, n, qout):
         p[2] = 0
         p[2, 4:8] = O.canon_to_mont_array([1])  # a zero point, skipped by pairing_batch
     many = parallel.pairing_many_distributed(p, q, compute=lambda a, b: O.pairing_many(a, b, 2))
+    import torch
+
+    def into(a, b, out):  # the device-resident form's per-shard compute, here on CPU tensors
+        res = O.pairing_many(a.numpy().view(np.uint64), b.numpy().view(np.uint64), 2)
+        out.copy_(torch.from_numpy(res.view(np.int64)))
+    many_dev = parallel.pairing_many_distributed_dev(torch.from_numpy(p.view(np.int64)),
+                                                     torch.from_numpy(q.view(np.int64)), compute=into)
+    assert np.array_equal(many_dev.numpy().view(np.uint64), many)
     mp_fn = lambda a, b: O.miller_loop_batch(b, a)[1]  # noqa: E731
     mul = lambda a, b: O.binary("orc_fq12_mul", a, b, 48, 48, 48)[0]  # noqa: E731
     def fe(f):

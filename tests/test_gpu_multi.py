@@ -62,3 +62,35 @@ def test_allgather_dev_world_of_one(data):
     ctx.pairing_many_allgather_dev([P.data_ptr()], [Q.data_ptr()], 101, [out.data_ptr()], [s.cuda_stream])
     torch.cuda.synchronize(dev)
     assert np.array_equal(out.cpu().numpy().view(np.uint64), data["gt"])
+
+
+def test_torch_distributed_forms_world_of_one(data):
+    """substrate_bn/parallel.py on the engine (no injected compute) under the nccl
+    backend (RCCL) as a world of one: the device-resident all-gather form and the
+    rank-ordered pairing_batch exchange equal the oracle bit for bit."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    from substrate_bn import parallel
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1, device_id=dev)
+    try:
+        P = torch.from_numpy(data["pz"].view(np.int64)).to(dev)
+        Q = torch.from_numpy(data["q"].view(np.int64)).to(dev)
+        got = parallel.pairing_many_distributed_dev(P, Q)
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(got.cpu().numpy().view(np.uint64), data["gt"])
+        st = torch.cuda.Stream(dev)
+        got2 = parallel.pairing_many_distributed_dev(P, Q, stream=st)
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(got2.cpu().numpy().view(np.uint64), data["gt"])
+        assert np.array_equal(parallel.pairing_batch_distributed(data["pz"], data["q"]), data["prod"])
+        assert np.array_equal(parallel.pairing_many_distributed(data["pz"], data["q"]), data["gt"])
+    finally:
+        dist.destroy_process_group()

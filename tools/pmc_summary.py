@@ -77,6 +77,11 @@ if cal.get("FETCH_SIZE") and cal.get("WRITE_SIZE"):
     print("calibration on k_fe_out: FETCH_SIZE/expected reads = %.3f, WRITE_SIZE/expected writes = %.3f"
           % (read_factor, write_factor))
 summary = {}
+# SURVEY.md 8(d) generic Fq-mul counts per element of the bench's kernels, and how many
+# elements one wave carries (the pairing path runs two lanes per pairing)
+ALG_FQMUL = {"k_pairing_fused": 19 + 2655 + 6045, "k_prepare": 19 + 2655, "k_miller": 6045, "k_fq12_vm": 8767,
+             "k_g1_mul": 3800, "k_g2_mul": 9165}
+ELEMS_PER_WAVE = {"k_pairing_fused": 32, "k_prepare": 32, "k_miller": 32, "k_fq12_vm": 32, "k_fe_out": 32}
 lines = ["%-16s %14s %14s %14s %12s %10s" % ("kernel", "FETCH_bytes", "WRITE_bytes", "VALU/wave", "WAVE_CYC/w",
                                                  "VALU/cyc")]
 for k, v in sorted(agg.items()):
@@ -89,10 +94,17 @@ for k, v in sorted(agg.items()):
     valu = m.get("SQ_INSTS_VALU", 0) / waves
     cyc = m.get("SQ_WAVE_CYCLES", 0) * 4 / waves  # quad-cycles -> cycles
     corr = (fetch / read_factor if read_factor else fetch) + write
+    # VALU lane-operations per algorithmic MAD32 (SURVEY 8(d) Fq-mul count x 128):
+    # wave-instructions x 64 lanes / elements per wave / algorithmic MADs per element
+    alg = ALG_FQMUL.get(k)
+    per_wave = ELEMS_PER_WAVE.get(k, 64)
+    valu_per_mad = valu * 64 / per_wave / (alg * 128) if alg else None
     summary[k] = {"hbm_bytes_per_launch": corr, "fetch_bytes_raw": fetch, "write_bytes": write,
                   "read_factor": read_factor, "write_factor": write_factor,
                   "valu_insts_per_wave": valu, "wave_cycles": cyc,
                   "valu_per_cycle_per_wave": valu / cyc if cyc else None,
+                  "algorithmic_fqmul_per_element": alg, "elements_per_wave": per_wave,
+                  "valu_lane_ops_per_algorithmic_mad": valu_per_mad,
                   "grbm_gui_active": m.get("GRBM_GUI_ACTIVE"),
                   "note": "FETCH_SIZE corrected by the read factor calibrated on k_fe_out (known bytes), "
                           "WRITE_SIZE as counted (MI355X_MICROARCH §HBM); source %s" % tag}
