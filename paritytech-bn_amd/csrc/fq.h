@@ -204,6 +204,60 @@ BN_INLINE Fq<kv(K)> fq_neg(const Fq<K>& a_in) {
     return fq_norm(Fq<kenc(B, 2)>{{r.v[0], r.v[1], r.v[2], r.v[3], r.v[4], r.v[5], r.v[6], r.v[7], r.v[8]}});
 }
 
+// ---------------------------------------------------------------- column accumulator
+// The digit products of several Fq products summed by columns in 17 64-bit
+// accumulators and reduced once (fq12_wide.h's twelve-product sums).  Measured
+// (profiles/r2n_wide_ubench_latency_forms.jsonl): for a SINGLE product this form is not
+// faster than the product-scanning fq_mul even on a lone wave (0.67 vs 0.62 us
+// per product in an inversion chain), so fq_mul keeps product scanning.
+struct Acc {
+    uint64_t c[17];
+};
+// t += x * y by columns: every column gains at most nine products < 2^58
+template <int A, int B>
+BN_INLINE void acc_mad(Acc& t, const Fq<A>& x, const Fq<B>& y) {
+    static_assert(kl(A) == 1 && kl(B) == 1, "acc_mad: normalized operands");
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) t.c[i + j] += (uint64_t)x.v[i] * y.v[j];
+}
+// one carry step on every column at once (independent, not a ripple): columns
+// end below 2^29 + 2^35, room for 54 more products before a reduction
+BN_INLINE void acc_carry_par(Acc& t) {
+    uint64_t h[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        h[k] = t.c[k] >> 29;
+        t.c[k] &= M29;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t.c[k + 1] += h[k];
+}
+// Montgomery reduction (R = 2^261) of the columns; each column plus the nine
+// m*p products it receives and a carry < 2^36 must stay below 2^64 (at most 54
+// products < 2^58 since the last acc_carry_par, or 54 in all).  BO: the
+// caller's output bound.
+template <int BO>
+BN_INLINE Fq<BO> acc_redc(Acc& t) {
+    Fq<BO> r;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        if (k) t.c[k] += t.c[k - 1] >> 29;
+        const uint32_t m = ((uint32_t)t.c[k] * BN_PINV29) & M29;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) t.c[k + j] += (uint64_t)m * kP29.v[j];
+    }
+    t.c[9] += t.c[8] >> 29;
+#pragma unroll
+    for (int k = 9; k < 16; ++k) {
+        r.v[k - 9] = (uint32_t)t.c[k] & M29;
+        t.c[k + 1] += t.c[k] >> 29;
+    }
+    r.v[7] = (uint32_t)t.c[16] & M29;
+    r.v[8] = (uint32_t)(t.c[16] >> 29);
+    return r;
+}
 // a * b * 2^-261 mod p: Montgomery product by finely integrated product
 // scanning.  Column k accumulates every a_i*b_j and m_i*p_j with i+j == k in a
 // 64-bit accumulator (9 products < La*Lb*2^58, 9 < 2^58 and the carry-in stay

@@ -81,49 +81,8 @@ __device__ __forceinline__ Fq<2> w_narrow(const Fq<K>& a) {
     if constexpr (kv(K) <= 2) return widen<2>(fq_norm(a)); else return fq_fold(a);
 }
 
-// ---------------------------------------------------------------- column accumulator
-// sum of digit products of several Fq products in 17 64-bit columns, carried
-// between batches and reduced once (Montgomery, R = 2^261)
-struct Acc {
-    uint64_t c[17];
-};
-template <int A, int B>
-__device__ __forceinline__ void acc_mad(Acc& t, const Fq<A>& x, const Fq<B>& y) {
-    static_assert(kl(A) == 1 && kl(B) == 1, "acc_mad: normalized operands");
-#pragma unroll
-    for (int i = 0; i < 9; ++i)
-#pragma unroll
-        for (int j = 0; j < 9; ++j) t.c[i + j] += (uint64_t)x.v[i] * y.v[j];
-}
-__device__ __forceinline__ void acc_carry(Acc& t) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        t.c[k + 1] += t.c[k] >> 29;
-        t.c[k] &= M29;
-    }
-}
-// REDC of carried columns holding a value <= U * p^2 (U = sum of the operand
-// bound products): result <= (U*p/2^261 + 1) * p
-template <int U>
-__device__ __forceinline__ auto acc_redc(Acc& t) {
-    constexpr int BO = 1 + (int)(((long long)U * 5908 + 999999) / 1000000);
-    Fq<BO> r;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        const uint32_t m = ((uint32_t)t.c[k] * BN_PINV29) & M29;
-#pragma unroll
-        for (int j = 0; j < 9; ++j) t.c[k + j] += (uint64_t)m * kP29.v[j];
-        t.c[k + 1] += t.c[k] >> 29;
-    }
-#pragma unroll
-    for (int k = 9; k < 16; ++k) {
-        t.c[k + 1] += t.c[k] >> 29;
-        r.v[k - 9] = (uint32_t)t.c[k] & M29;
-    }
-    r.v[7] = (uint32_t)t.c[16] & M29;
-    r.v[8] = (uint32_t)(t.c[16] >> 29);
-    return r;
-}
+// The twelve-product sums use the column accumulator of fq.h (Acc, acc_mad,
+// acc_carry_par, acc_redc).
 
 // ---------------------------------------------------------------- operations
 // this lane's coordinate of xi * (the lane pair's Fq2), xi = 9 + u (fq2.rs:19-34)
@@ -154,10 +113,10 @@ __device__ __noinline__ Fq<2> w12_mul(Fq<2> a, Fq<2> b) {
         const Fq<2> yx = w_get<2>(w.c ? B_ : N_, 2 * j + 1 - w.c);
         acc_mad(t, x0, yo);
         acc_mad(t, x1, yx);
-        if (i == 2) acc_carry(t);  // six normalized products per batch keep columns < 2^64
+        if (i == 2) acc_carry_par(t);  // six normalized products per batch keep columns < 2^64
     }
-    acc_carry(t);
-    return acc_redc<12 * 2 * 2>(t);
+    // value <= 12 * (2p)^2: the result is below (48 p / 2^261 + 1) p < 2p
+    return acc_redc<2>(t);
 }
 
 // Granger-Scott cyclotomic squaring (fq12.rs:198-247).  Pairs (z0,z1), (z2,z3),
