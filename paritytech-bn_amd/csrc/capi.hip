@@ -1054,7 +1054,7 @@ int bn_gt_pow_many_dev(bn_ctx* c, const bn_gt* d_a, const bn_fr* d_k, size_t n, 
     WsUse use{c, s};
     for (size_t off = 0; off < n; off += kChunk) {
         const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
-        KL(k_gt_pow, d_a + off, d_k + off, m, d_out + off, c->slots);
+        k_gt_pow<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_a + off, d_k + off, m, d_out + off, c->slots);
         HIPCHK(c, hipGetLastError());
     }
     return BN_OK;
@@ -1064,7 +1064,8 @@ int bn_gt_pow_many(bn_ctx* c, const bn_gt* a, const bn_fr* k, size_t n, bn_gt* o
     return staged(c, n, {{a, sizeof(bn_gt)}, {k, sizeof(bn_fr)}}, {{out, sizeof(bn_gt)}},
                   [&](void** d, size_t m, hipStream_t s) -> int {
                       RET_IF(reserve(c, m));
-                      KL(k_gt_pow, (const bn_gt*)d[0], (const bn_fr*)d[1], m, (bn_gt*)d[2], c->slots);
+                      k_gt_pow<<<grid_for(kPathLanes * m), kBlock, 0, s>>>((const bn_gt*)d[0], (const bn_fr*)d[1], m, (bn_gt*)d[2],
+                                                                         c->slots);
                       return BN_OK;
                   });
 }

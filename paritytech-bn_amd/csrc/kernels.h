@@ -153,6 +153,15 @@ __device__ __forceinline__ Fq12<B> ld_fq12_buf_sel(const uint32_t* ws, size_t n,
     auto q = [&](int k) { return Fq2<B>{ld_fq_buf<B>(rs, vo, n, 2 * k), ld_fq_buf<B>(rs, vo, n, 2 * k + 1)}; };
     return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
 }
+#else
+// two lanes per element: `n` counts lanes, the lane's own coordinates
+template <int B>
+__device__ __forceinline__ Fq12<B> ld_fq12_buf_sel(const uint32_t* ws, size_t n, uint32_t vo_bytes) {
+    const auto rs = slot_rsrc(ws);
+    const int vo = (int)vo_bytes;
+    auto q = [&](int k) { return Fq2<B>{ld_fq_buf<B>(rs, vo, n, k)}; };
+    return {{q(0), q(1), q(2)}, {q(3), q(4), q(5)}};
+}
 #endif
 
 template <int B>

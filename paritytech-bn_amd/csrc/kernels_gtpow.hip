@@ -1,12 +1,15 @@
 // kernels_gtpow.hip -- batched Gt::pow(Fr) (lib.rs:592-594 -> generic Fq12 pow,
-// fields/mod.rs:35-46), one lane per power.
+// fields/mod.rs:35-46), on the pairing path's two-lane layout (BN_PATH_SPLIT,
+// fq2_split.h: each lane holds one coordinate of every Fq2, so 2^16 powers are
+// 2,048 waves, two per SIMD).
 //
 // The reference squares-and-multiplies over all 256 bits of U256::from(Fr)
 // with the generic Fq12 square (the input need not lie in the cyclotomic
 // subgroup: a Gt may hold a miller_loop_batch value), so this does too, with a
-// fixed 4-bit window: a per-lane table x^0..x^15 in lane-strided HBM slots,
+// fixed 4-bit window: a per-element table x^0..x^15 in lane-strided HBM slots,
 // 252 generic squarings and 63 products by a table entry.  x^e is unique, so
-// the canonical output equals the reference's.
+// the canonical output equals the reference's.  Both lanes of an element hold
+// the same scalar and select the same entry.
 //
 // The table entry is selected per lane through the VGPR offset of a buffer
 // descriptor built from the uniform workspace base (ld_fq12_buf_sel): the
@@ -17,37 +20,42 @@
 #ifndef BN_FOLD_LDS
 #define BN_FOLD_LDS 1
 #endif
+#include "fq.h"
+#define BN_SPLIT BN_PATH_SPLIT
 #include "kernels.h"
 
 namespace bn {
 
-__global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, const bn_fr* __restrict__ k, size_t n,
-                                                   bn_gt* __restrict__ out, uint32_t* __restrict__ ws) {
+constexpr size_t kL = BN_SPLIT ? 2 : 1;  // lanes per element in this translation unit
+
+__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a,
+                                                               const bn_fr* __restrict__ k, size_t n,
+                                                               bn_gt* __restrict__ out, uint32_t* __restrict__ ws) {
     fold_table_init();
-    const size_t i = lane_id();
+    const size_t l = lane_id(), i = l / kL;
     if (i >= n) return;
-    // slot access through a buffer descriptor with the stride laundered per use
-    // (kernels.h, as in the step machine): no hoisted per-word offsets
-    auto slot = [&](uint32_t t, size_t nn) { return ws + (size_t)t * kSlotWords * nn; };
+    // slot access through a buffer descriptor with the lane stride laundered per
+    // use (kernels.h, as in the step machine): no hoisted per-word offsets
+    auto slot = [&](uint32_t t, size_t nn) { return ws + (size_t)t * kSlotLaneWords * nn; };
     auto stride = [&]() {
-        size_t nn = n;
+        size_t nn = kL * n;
         asm volatile("" : "+s"(nn));
         return nn;
     };
-    // byte offset of lane i's copy of table entry t (t is per lane)
-    auto sel = [&](uint32_t t, size_t nn) { return (uint32_t)(((size_t)t * kSlotWords * nn + i) * 4); };
+    // byte offset of lane l's copy of table entry t (t is per element)
+    auto sel = [&](uint32_t t, size_t nn) { return (uint32_t)(((size_t)t * kSlotLaneWords * nn + l) * 4); };
     const Fq12<kF> x = widen<kF>(ld_gt(a[i]));
     {
         const size_t nn = stride();
-        st_fq12_buf(slot(0, nn), nn, i, widen<kF>(fq12_one()));
-        st_fq12_buf(slot(1, nn), nn, i, x);
+        st_fq12_buf(slot(0, nn), nn, l, widen<kF>(fq12_one()));
+        st_fq12_buf(slot(1, nn), nn, l, x);
     }
     Fq12<kF> t = x;
 #pragma unroll 1
     for (uint32_t j = 2; j < 16; ++j) {
         const size_t nn = stride();
-        t = mul12(t, ld_fq12_buf<kF>(slot(1, nn), nn, i));
-        st_fq12_buf(slot(j, nn), nn, i, t);
+        t = mul12(t, ld_fq12_buf<kF>(slot(1, nn), nn, l));
+        st_fq12_buf(slot(j, nn), nn, l, t);
     }
     uint32_t e[8];
     fr_to_canonical(k[i], e);  // U256::from(Fr), fp.rs:13-20
