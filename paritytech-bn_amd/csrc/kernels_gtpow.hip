@@ -7,9 +7,10 @@
 // with the generic Fq12 square (the input need not lie in the cyclotomic
 // subgroup: a Gt may hold a miller_loop_batch value), so this does too, with a
 // fixed 4-bit window: a per-element table x^0..x^15 in lane-strided HBM slots,
-// 252 generic squarings and 63 products by a table entry.  x^e is unique, so
-// the canonical output equals the reference's.  Both lanes of an element hold
-// the same scalar and select the same entry.
+// 252 squarings and 63 products by a table entry (the squarings cyclotomic when
+// the whole wave holds cyclotomic-subgroup members, see below).  x^e is unique,
+// so the canonical output equals the reference's.  Both lanes of an element
+// hold the same scalar and select the same entry.
 //
 // The table entry is selected per lane through the VGPR offset of a buffer
 // descriptor built from the uniform workspace base (ld_fq12_buf_sel): the
@@ -20,6 +21,8 @@
 #ifndef BN_FOLD_LDS
 #define BN_FOLD_LDS 1
 #endif
+#include <type_traits>
+
 #include "fq.h"
 #define BN_SPLIT BN_PATH_SPLIT
 #include "kernels.h"
@@ -27,6 +30,20 @@
 namespace bn {
 
 constexpr size_t kL = BN_SPLIT ? 2 : 1;  // lanes per element in this translation unit
+
+// True when every element of the wave is a nonzero member of the cyclotomic
+// subgroup (order p^4 - p^2 + 1, where every pairing output lies):
+// x^(p^4) * x == x^(p^2).  There the Granger-Scott square (fq12.rs:198-247,
+// tower.h fq12_cyclotomic_sqr) equals the generic square as a field element, at
+// half its cost, so the power -- and its canonical image -- is unchanged.  The
+// choice is wave-uniform: one non-member (a Miller value, say) sends its whole
+// wave down the generic chain, and lanes never diverge.
+__device__ __forceinline__ bool gt_pow_wave_cyclotomic(const Fq12<kF>& x) {
+    const Fq12<kF> x2 = narrow12<kF>(fq12_frobenius_map<2>(x));
+    const Fq12<kF> x4x = mul12(narrow12<kF>(fq12_frobenius_map<2>(x2)), x);
+    const bool member = fq12_is_zero(fq12_sub(x4x, x2)) & !fq12_is_zero(x);
+    return __all(member);
+}
 
 __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a,
                                                                const bn_fr* __restrict__ k, size_t n,
@@ -57,24 +74,35 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __r
         t = mul12(t, ld_fq12_buf<kF>(slot(1, nn), nn, l));
         st_fq12_buf(slot(j, nn), nn, l, t);
     }
-    uint32_t e[8];
-    fr_to_canonical(k[i], e);  // U256::from(Fr), fp.rs:13-20
-    Fq12<kF> acc;
-    {
-        const size_t nn = stride();
-        acc = ld_fq12_buf_sel<kF>(ws, nn, sel(e[7] >> 28, nn));
-    }
-#pragma unroll 1
-    for (int w = 62; w >= 0; --w) {
+    uint32_t e0[8];
+    fr_to_canonical(k[i], e0);  // U256::from(Fr), fp.rs:13-20
+    // 63 windows of four squarings and one table product; Cyc selects the square
+    auto chain = [&](auto cyc) {
+        uint32_t e[8];
 #pragma unroll
-        for (int s = 7; s > 0; --s) e[s] = (e[s] << 4) | (e[s - 1] >> 28);
-        e[0] <<= 4;
+        for (int s = 0; s < 8; ++s) e[s] = e0[s];
+        Fq12<kF> acc;
+        {
+            const size_t nn = stride();
+            acc = ld_fq12_buf_sel<kF>(ws, nn, sel(e[7] >> 28, nn));
+        }
 #pragma unroll 1
-        for (int s = 0; s < 4; ++s) acc = narrow12<kF>(fq12_sqr(acc));
-        const size_t nn = stride();
-        acc = mul12(acc, ld_fq12_buf_sel<kF>(ws, nn, sel(e[7] >> 28, nn)));
-    }
-    st_gt(out[i], acc);
+        for (int w = 62; w >= 0; --w) {
+#pragma unroll
+            for (int s = 7; s > 0; --s) e[s] = (e[s] << 4) | (e[s - 1] >> 28);
+            e[0] <<= 4;
+#pragma unroll 1
+            for (int s = 0; s < 4; ++s) {
+                if constexpr (decltype(cyc)::value) acc = cyc_sqr(acc);
+                else acc = narrow12<kF>(fq12_sqr(acc));
+            }
+            const size_t nn = stride();
+            acc = mul12(acc, ld_fq12_buf_sel<kF>(ws, nn, sel(e[7] >> 28, nn)));
+        }
+        return acc;
+    };
+    if (gt_pow_wave_cyclotomic(x)) st_gt(out[i], chain(std::true_type{}));
+    else st_gt(out[i], chain(std::false_type{}));
 }
 
 }  // namespace bn

@@ -54,22 +54,29 @@ void he_fq12_mul_by_024(const uint32_t* f, const uint32_t* e0, const uint32_t* e
     st12(fq12_mul_by_024(ld12(f), ld2(e0), ld2(evw), ld2(evv)), o);
 }
 // k_gt_pow's formulas (kernels_gtpow.hip): 4-bit window table x^0..x^15, then
-// 63 windows of four generic squarings and one product; e = canonical scalar words
-void he_gt_pow(const uint32_t* a, const uint32_t* e_in, uint32_t* o) {
+// 63 windows of four squarings and one product; e = canonical scalar words.  The
+// squarings are cyclotomic when x is a nonzero cyclotomic-subgroup member
+// (x^(p^4) * x == x^(p^2)), as for a whole wave of such elements on the device.
+// Returns 1 when the cyclotomic chain ran.
+int he_gt_pow(const uint32_t* a, const uint32_t* e_in, uint32_t* o) {
     Fq12<kF> tab[16];
     tab[0] = widen<kF>(fq12_one());
     tab[1] = widen<kF>(ld12(a));
     for (int j = 2; j < 16; ++j) tab[j] = mul12(tab[j - 1], tab[1]);
+    const Fq12<kF> x2 = narrow12<kF>(fq12_frobenius_map<2>(tab[1]));
+    const Fq12<kF> x4x = mul12(narrow12<kF>(fq12_frobenius_map<2>(x2)), tab[1]);
+    const bool cyc = fq12_is_zero(fq12_sub(x4x, x2)) && !fq12_is_zero(tab[1]);
     uint32_t e[8];
     memcpy(e, e_in, sizeof e);
     Fq12<kF> acc = tab[e[7] >> 28];
     for (int w = 62; w >= 0; --w) {
         for (int s = 7; s > 0; --s) e[s] = (e[s] << 4) | (e[s - 1] >> 28);
         e[0] <<= 4;
-        for (int s = 0; s < 4; ++s) acc = narrow12<kF>(fq12_sqr(acc));
+        for (int s = 0; s < 4; ++s) acc = cyc ? cyc_sqr(acc) : narrow12<kF>(fq12_sqr(acc));
         acc = mul12(acc, tab[e[7] >> 28]);
     }
     st12(acc, o);
+    return cyc;
 }
 void he_final_exp(const uint32_t* f, uint32_t* o) {
     st12(fe_last_chunk(fe_first_chunk(widen<kF>(ld12(f)))), o);

@@ -28,8 +28,9 @@ def lib():
     return _lib
 
 
-def call(name, *arrays, out_words, ints=()):
-    """arrays: uint64 memory images; returns uint64 output of out_words*... u32 words."""
+def call(name, *arrays, out_words, ints=(), ret=False):
+    """arrays: uint64 memory images; returns the uint64 output of out_words u32
+    words (and the function's int result with ret=True)."""
     fn = getattr(lib(), name)
     args = []
     keep = []
@@ -40,5 +41,5 @@ def call(name, *arrays, out_words, ints=()):
     out = np.zeros(out_words // 2, dtype=np.uint64)
     args = args[:1] + [ctypes.c_int(i) for i in ints] + args[1:] if ints else args
     args.append(out.ctypes.data_as(ctypes.c_void_p))
-    fn(*args)
-    return out
+    rc = fn(*args)
+    return (out, rc) if ret else out

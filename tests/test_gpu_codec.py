@@ -144,6 +144,12 @@ def test_gt_pow(ctx):
     k[2] = O.canon_to_mont_array([R - 1], O.FR)
     out = ctx.gt_pow_many(a, k)
     assert np.array_equal(out, O.gt_pow(a, k))
+    # waves holding only pairing outputs take the cyclotomic squarings, the rest the
+    # generic ones: a Miller value and a zero element inside an otherwise cyclotomic wave
+    b = np.concatenate([g[:10], ml[:1], g[10:40], np.zeros((1, 48), np.uint64), g[40:], ml[1:]])
+    kb = np.concatenate([k, k[:1]])
+    out = ctx.gt_pow_many(b, kb)
+    assert np.array_equal(out, O.gt_pow(b, kb))
 
 
 def test_rust_api_mirror_codec(kats):

@@ -64,7 +64,8 @@ def test_tower_vs_oracle(rnd):
 
 
 def test_gt_pow_formulas():
-    # k_gt_pow's window chain on a pairing output and a (non-cyclotomic) Miller value
+    # k_gt_pow's window chain on a pairing output (cyclotomic squarings) and a
+    # (non-cyclotomic) Miller value (generic squarings)
     p, q, _, _ = O.random_pairs(2, seed=61)
     a = np.concatenate([O.pairing_many(p[:1], q[:1]), O.miller_loop_batch(q[1:2], p[1:2])[1][None]])
     vals, k = O.random_scalars(2, 62, lo=0)
@@ -72,7 +73,8 @@ def test_gt_pow_formulas():
         K = O.canon_to_mont_array([scal], O.FR).reshape(1, 4)
         words = np.frombuffer(int(scal).to_bytes(32, "little"), np.uint64).copy()
         for j in range(2):
-            got = H.call("he_gt_pow", a[j], words, out_words=96)
+            got, cyc = H.call("he_gt_pow", a[j], words, out_words=96, ret=True)
+            assert cyc == (j == 0)  # the pairing output takes the cyclotomic chain, the Miller value not
             assert np.array_equal(got, O.gt_pow(a[j:j + 1], K)[0])
 
 
