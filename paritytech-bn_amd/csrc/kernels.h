@@ -20,8 +20,11 @@ constexpr int kPathLanes = BN_PATH_SPLIT ? 2 : 1;
 // words of one Fq12 slot per lane of the translation unit's own layout
 constexpr int kSlotLaneWords = BN_SPLIT ? 54 : 108;
 #if BN_SPLIT
-// two waves per SIMD: the kernel must fit 256 registers
-#define BN_PATH_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
+// two waves per SIMD: the kernel must fit 256 registers (BN_PATH_WAVES: A/B builds)
+#ifndef BN_PATH_WAVES
+#define BN_PATH_WAVES 2
+#endif
+#define BN_PATH_ATTR __attribute__((amdgpu_waves_per_eu(BN_PATH_WAVES, BN_PATH_WAVES)))
 #else
 #define BN_PATH_ATTR
 #endif
