@@ -507,12 +507,12 @@ int bn_ctx_destroy(bn_ctx* c) {
     if (c->ws_event) (void)hipEventDestroy(c->ws_event);
     for (void* p : {(void*)c->coeffs, (void*)c->paff, (void*)c->slots, (void*)c->flags, (void*)c->d_err,
                     (void*)c->d_prog, c->stage})
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
     for (auto& ev : c->ev_marks)
         for (auto e : ev) c->ev_pool.push_back(e);
     for (auto e : c->ev_pool)
-        if (e) hipEventDestroy(e);
-    hipStreamDestroy(c->stream);
+        if (e) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
     delete c;
     return BN_OK;
 }
@@ -555,7 +555,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
         if (c->timing)
             for (auto& e : ev) e = take_event(c);
         auto mark = [&](int k) {
-            if (c->timing && ev[k]) hipEventRecord(ev[k], s);
+            if (c->timing && ev[k]) (void)hipEventRecord(ev[k], s);
         };
         mark(0);
         if (m <= c->fe_wide_max) {

@@ -306,8 +306,54 @@ BN_INLINE auto fq_mul(const Fq<A>& a_in, const Fq<B>& b_in) {
     return r;
     }
 }
+// a^2 * 2^-261 mod p: fq_mul's column scan with each cross product a_i*a_j
+// (i < j) taken once against the doubled digit 2*a_j, so a column holds at most
+// four cross products (< 2L^2 * 2^58 each), one square and nine m*p terms:
+// 45 + 81 digit products instead of 81 + 81.  The same residue as fq_mul(a, a).
+#ifndef BN_FQ_SQR
+#define BN_FQ_SQR 1
+#endif
 template <int B>
-BN_INLINE auto fq_sqr(const Fq<B>& a) { return fq_mul(a, a); }
+BN_INLINE auto fq_sqr(const Fq<B>& a_in) {
+#if BN_FQ_SQR
+    if constexpr (kl(B) > 2) {
+        return fq_sqr(fq_norm(a_in));
+    } else {
+    static_assert((long long)kv(B) * kv(B) <= 160 * 160, "product bound");
+    static_assert(kl(B) * kl(B) * 9 + 9 + 1 < 64, "fq_sqr: column sum could overflow 64 bits");
+    const Fq<B>& a = a_in;
+    uint32_t d[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
+    uint32_t m[9];
+    Fq<mul_bound(kv(B), kv(B))> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+        const int lo = k < 9 ? 0 : k - 8;
+        const int hi = k < 9 ? k : 8;
+#pragma unroll
+        for (int i = lo; i <= hi; ++i) {
+            const int j = k - i;
+            if (i < j) acc += (uint64_t)a.v[i] * d[j];
+            else if (i == j) acc += (uint64_t)a.v[i] * a.v[i];
+            if (i < k) acc += (uint64_t)m[i] * kP29.v[k - i];
+        }
+        if (k < 9) {
+            m[k] = ((uint32_t)acc * BN_PINV29) & M29;
+            acc += (uint64_t)m[k] * kP29.v[0];
+        } else {
+            r.v[k - 9] = (uint32_t)acc & M29;
+        }
+        acc >>= 29;
+    }
+    r.v[8] = (uint32_t)acc;
+    return r;
+    }
+#else
+    return fq_mul(a_in, a_in);
+#endif
+}
 
 // bring any value back to bound 2 (a Montgomery product with one)
 template <int B>
