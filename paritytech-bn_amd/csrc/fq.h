@@ -177,14 +177,19 @@ constexpr Limbs9 kp_spread(int K, int L) {
 // the normalized digits of K*p
 constexpr Limbs9 kp_plain(int K) { return kp_spread(K, -1); }
 
-// a - b + (B+1)*p, lazy (arith.rs:290-296 computes the same residue)
+// digit headroom kp_spread needs to subtract a value of digit bound L: one
+// 2^29 per digit covers a normalized subtrahend (digits <= 2^29 - 1), else L
+constexpr int sub_spread(int L) { return L == 1 ? 0 : L; }
+
+// a - b + (B+1)*p, lazy (arith.rs:290-296 computes the same residue); digits
+// < (La + sub_spread(Lb) + 2) * 2^29
 template <int A, int B>
 BN_INLINE auto fq_sub(const Fq<A>& a, const Fq<B>& b) {
-    if constexpr (kl(A) + kl(B) + 2 > kMaxLimb) {
+    if constexpr (kl(A) + sub_spread(kl(B)) + 2 > kMaxLimb) {
         if constexpr (kl(A) >= kl(B)) return fq_sub(fq_norm(a), b); else return fq_sub(a, fq_norm(b));
     } else {
-        constexpr Limbs9 Q = kp_spread(kv(B) + 1, kl(B));
-        Fq<kenc(kv(A) + kv(B) + 1, kl(A) + kl(B) + 2)> r;
+        constexpr Limbs9 Q = kp_spread(kv(B) + 1, sub_spread(kl(B)));
+        Fq<kenc(kv(A) + kv(B) + 1, kl(A) + sub_spread(kl(B)) + 2)> r;
 #pragma unroll
         for (int i = 0; i < 9; ++i) r.v[i] = (a.v[i] + Q.v[i]) - b.v[i];
         return r;

@@ -105,11 +105,11 @@ BN_INLINE void fq2_fence(Fq2<B>& a) {
 #endif
 }
 
-// K*p - x without a carry pass (digits < (L+2)*2^29, value <= (B+1)*p)
+// K*p - x without a carry pass (digits < (sub_spread(L)+2)*2^29, value <= (B+1)*p)
 template <int K>
-BN_INLINE Fq<kenc(kv(K) + 1, kl(K) + 2)> fq_neg_lazy(const Fq<K>& x) {
-    constexpr Limbs9 Q = kp_spread(kv(K) + 1, kl(K));
-    Fq<kenc(kv(K) + 1, kl(K) + 2)> r;
+BN_INLINE Fq<kenc(kv(K) + 1, sub_spread(kl(K)) + 2)> fq_neg_lazy(const Fq<K>& x) {
+    constexpr Limbs9 Q = kp_spread(kv(K) + 1, sub_spread(kl(K)));
+    Fq<kenc(kv(K) + 1, sub_spread(kl(K)) + 2)> r;
 #pragma unroll
     for (int i = 0; i < 9; ++i) r.v[i] = Q.v[i] - x.v[i];
     return r;
@@ -160,10 +160,15 @@ BN_INLINE auto fq_dot2(const Fq<X>& x, const Fq<Y>& y, const Fq<Z>& z, const Fq<
 // fq2.rs:136-148 (the same residues as fq2_mul_sb): lane 0 computes
 // c0 = a0*b0 + a1*(K*p - b1), lane 1 computes c1 = a1*b0 + a0*b1, both as
 // own_a * Y + partner_a * W with per-lane operand choice.
+// the fq_dot2 column budget of fq2_mul_split(a, b) for digit bounds La, Lb: x = a,
+// y = b or its partner (Lb), z = partner of a (La), w = b or K*p - partner (fq_neg_lazy)
+constexpr int split_mul_cost(int La, int Lb) {
+    return La * Lb + La * (Lb > sub_spread(Lb) + 2 ? Lb : sub_spread(Lb) + 2);
+}
 template <int A, int B>
 BN_INLINE auto fq2_mul_split(const Fq2<A>& a, const Fq2<B>& b) {
-    if constexpr (kl(A) * (2 * kl(B) + 2) > 6) {
-        if constexpr (kl(B) * (2 * kl(A) + 2) <= 6) return fq2_mul_split(b, a);
+    if constexpr (split_mul_cost(kl(A), kl(B)) > 6) {
+        if constexpr (split_mul_cost(kl(B), kl(A)) <= 6) return fq2_mul_split(b, a);
         else if constexpr (kl(A) >= kl(B)) return fq2_mul_split(fq2_norm(a), b);
         else return fq2_mul_split(a, fq2_norm(b));
     } else {
@@ -214,7 +219,8 @@ BN_INLINE auto fq2_mul2(const Fq2<A>& a_in, const Fq2<B>& b_in, const Fq2<C>& c_
 }
 
 // fq2.rs:105-117: c0 = (a0 - a1)(a0 + a1), c1 = 2*a0*a1 -- one product per lane:
-// lane 0: (a0 + K*p - a1) * (a0 + a1), lane 1: a1 * (2*a0)
+// lane 0: (a0 + K*p - a1) * (a0 + a1), lane 1: a1 * (a0 + a0).  x keeps digits
+// below 3*2^29 (no carry pass: fq_mul takes a 3 x 2 digit-bound product).
 template <int A>
 BN_INLINE auto fq2_sqr(const Fq2<A>& a_in) {
     if constexpr (kv(A) > 40) return fq2_sqr(fq2_fold(a_in)); else {
@@ -223,8 +229,8 @@ BN_INLINE auto fq2_sqr(const Fq2<A>& a_in) {
     const bool odd = lane_odd();
     const Fq<kv(A)> own = fq_norm(a.c);
     const Fq<kv(A)> par = fq_partner(own);
-    const auto x = fq_norm(fq_pick(odd, own, fq_sub(own, par)));
-    const auto y = fq_pick(odd, fq_add(par, par), fq_add(own, par));
+    const auto x = fq_pick(odd, own, fq_sub(own, par));
+    const auto y = fq_add(par, fq_select(odd, par, own));
     auto r = wrap2(fq_mul(x, y));
     fq2_fence(r);
     return r;

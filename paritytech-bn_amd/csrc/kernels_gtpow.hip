@@ -41,7 +41,7 @@ constexpr size_t kL = BN_SPLIT ? 2 : 1;  // lanes per element in this translatio
 __device__ __forceinline__ bool gt_pow_wave_cyclotomic(const Fq12<kF>& x) {
     const Fq12<kF> x2 = narrow12<kF>(fq12_frobenius_map<2>(x));
     const Fq12<kF> x4x = mul12(narrow12<kF>(fq12_frobenius_map<2>(x2)), x);
-    const bool member = fq12_is_zero(fq12_sub(x4x, x2)) & !fq12_is_zero(x);
+    const bool member = ((unsigned)fq12_is_zero(fq12_sub(x4x, x2)) & (unsigned)!fq12_is_zero(x)) != 0;
     return __all(member);
 }
 

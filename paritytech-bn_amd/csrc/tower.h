@@ -479,7 +479,9 @@ BN_INLINE Fq6<2> fq6_fold(const Fq6<B>& a) {
 template <int B>
 BN_INLINE Fq6<kv(B)> fq6_norm(const Fq6<B>& a) { return {fq2_norm(a.c0), fq2_norm(a.c1), fq2_norm(a.c2)}; }
 template <int B>
-BN_INLINE bool fq6_is_zero(const Fq6<B>& a) { return fq2_is_zero(a.c0) & fq2_is_zero(a.c1) & fq2_is_zero(a.c2); }
+BN_INLINE bool fq6_is_zero(const Fq6<B>& a) {
+    return ((unsigned)fq2_is_zero(a.c0) & (unsigned)fq2_is_zero(a.c1) & (unsigned)fq2_is_zero(a.c2)) != 0;  // no branches
+}
 template <int L, int B>
 BN_INLINE auto pre(const Fq6<B>& a) {
     if constexpr (kv(B) <= L) return a; else return fq6_fold(a);
@@ -577,7 +579,7 @@ BN_INLINE Fq12<2> fq12_fold(const Fq12<B>& a) { return {fq6_fold(a.c0), fq6_fold
 template <int B>
 BN_INLINE Fq12<kv(B)> fq12_norm(const Fq12<B>& a) { return {fq6_norm(a.c0), fq6_norm(a.c1)}; }
 template <int B>
-BN_INLINE bool fq12_is_zero(const Fq12<B>& a) { return fq6_is_zero(a.c0) & fq6_is_zero(a.c1); }
+BN_INLINE bool fq12_is_zero(const Fq12<B>& a) { return ((unsigned)fq6_is_zero(a.c0) & (unsigned)fq6_is_zero(a.c1)) != 0; }
 template <int L, int B>
 BN_INLINE auto pre(const Fq12<B>& a) {
     if constexpr (kv(B) <= L) return a; else return fq12_fold(a);
@@ -697,12 +699,12 @@ BN_INLINE auto fq12_cyclotomic_sqr(const Fq12<A>& a) {
     auto t2 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z2, z3), fq2_add(fq2_mul_xi(z3), z2)), tmp23), fq2_mul_xi(tmp23)));
     auto t3 = fq2_dbl(tmp23);
     auto tmp45 = fq2_mul(z4, z5);
-    auto t4 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z4, z5), fq2_add(fq2_mul_xi(z5), z4)), tmp45), fq2_mul_xi(tmp45)));
-    auto t5 = fq2_dbl(tmp45);
+    auto xi45 = fq2_mul_xi(tmp45);  // also gives xi * t5 = 2 * xi * tmp45 below
+    auto t4 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z4, z5), fq2_add(fq2_mul_xi(z5), z4)), tmp45), xi45));
 
     auto n0 = fq2_add(fq2_dbl(fq2_sub(t0, z0)), t0);
     auto n1 = fq2_add(fq2_dbl(fq2_add(t1, z1)), t1);
-    auto x5 = fq2_fold(fq2_mul_xi(t5));
+    auto x5 = fq2_fold(fq2_dbl(xi45));  // xi * t5
     auto n2 = fq2_add(fq2_dbl(fq2_add(x5, z2)), x5);
     auto n3 = fq2_add(fq2_dbl(fq2_sub(t4, z3)), t4);
     auto n4 = fq2_add(fq2_dbl(fq2_sub(t2, z4)), t2);
