@@ -55,7 +55,7 @@ __device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p
     // and qz^-1 = conj(qz) * (t * pz).  Inverses are unique: these are the values the
     // reference's two inversions give.  A zero z makes t = 0; that pair is skipped
     // (flags) or rejected (mode 1) and its values are never used.
-    const Fq<2> t = fq_inv_w(fq_mul(pz, nq));
+    const Fq<2> t = fq_inv(fq_mul(pz, nq));
     const auto pzinv = fq_mul(t, nq);
     const auto ninv = fq_mul(t, pz);
     auto pzinv2 = fq_sqr(pzinv);

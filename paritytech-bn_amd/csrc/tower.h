@@ -29,6 +29,10 @@ namespace bn {
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
+#ifndef BN_INV_BGCD
+#define BN_INV_BGCD 1  // fq_inv: binary GCD (1) or the Fermat chain (0)
+#endif
+
 // ---------------------------------------------------------------- inversion
 // Fermat: a^(p-2).  Inverses are unique, so this equals the reference's binary
 // extended Euclid (arith.rs:324-370 + fp.rs:108-117) bit for bit, without its
@@ -123,8 +127,160 @@ BN_INLINE Fq<2> fq_pow_plan(const Fq<B>& a, const PowPlan& c) {
 // instead of the binary chain's ~126): the same unique inverse
 template <int B>
 BN_INLINE Fq<2> fq_inv_w(const Fq<B>& a) { return fq_pow_plan(a, kInvPlan); }
+
+// ---------------------------------------------------------------- binary-GCD inversion
+// Pornin's optimized binary GCD ("Optimized Binary GCD for Modular Inversion",
+// 2020, Algorithm 2) with 29-bit steps to match the digit size: each outer
+// round runs 29 binary-GCD steps on 60-bit approximations of (a, b) -- their
+// low 29 bits exact, the top 31 bits of max(len(a), len(b), 60) -- collecting
+// the update factors (f0, g0, f1, g1), |f| + |g| <= 2^29, then applies them to
+// the full (a, b) (exact division by 2^29, sign fixes) and to (u, v) with a
+// Montgomery division by 2^29 (add k*p, drop the low digit), which keeps
+// a == y*u and b == y*v (mod p).  ceil((2*254 - 1)/29) = 18 rounds reach b = 1,
+// so v = y^-1; one spare round (a no-op once a = 0).  No data-dependent branch:
+// every lane runs the same instructions.  About a third of the instructions of
+// the Fermat chain (253 squarings).  y^-1 is unique, so the value equals the
+// reference's binary extended Euclid (arith.rs:324-370) bit for bit.
+#ifndef BN_INV_ROUNDS
+#define BN_INV_ROUNDS 19
+#endif
+constexpr int kInvRounds = BN_INV_ROUNDS;
+constexpr Limbs9 kR3 = {{0x0e2312b2u, 0x16c05ca2u, 0x0bc84389u, 0x1cdf310bu, 0x11adafddu, 0x032e568eu, 0x1d6ae48cu,
+                         0x10d4cd1fu, 0x0026c2d2u}};  // 2^783 mod p: REDC(v * R^3) = v * R^2
+// (x*f0 + y*g0) / 2^29 for the exact (a, b) update: the low digit cancels; the
+// result comes back with the sign removed (m: all ones when it was negative)
+BN_INLINE uint32_t bgcd_lin_exact(const uint32_t (&x)[9], const uint32_t (&y)[9], int32_t f, int32_t g,
+                                  uint32_t (&r)[9]) {
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const int64_t t = (int64_t)(int32_t)x[i] * f + (int64_t)(int32_t)y[i] * g + c;
+        if (i) r[i - 1] = (uint32_t)t & M29;
+        c = t >> 29;
+    }
+    r[8] = (uint32_t)c;  // signed top digit
+    const uint32_t m = (uint32_t)((int32_t)r[8] >> 31);
+    // conditional negation, carried: -X = sum (-d_i) 2^(29 i)
+    int64_t cn = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int64_t t = (int64_t)(int32_t)((r[i] ^ m) - m) + cn;
+        r[i] = (uint32_t)t & M29;
+        cn = t >> 29;
+    }
+    r[8] = (uint32_t)((int64_t)(int32_t)((r[8] ^ m) - m) + cn);
+    return m;
+}
+// (x*f + y*g) / 2^29 mod p for the (u, v) update: + k*p clears the low digit,
+// + 3p (|x f + y g| / 2^29 < 2p for x, y < 2p, and k*p / 2^29 < p) keeps every
+// digit non-negative; the result is < 6p, normalized
+BN_INLINE Fq<6> bgcd_lin_mont(const Fq<2>& x, const Fq<2>& y, int32_t f, int32_t g) {
+    constexpr Limbs9 P3 = kp_plain(3);
+    int64_t t[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t[i] = (int64_t)(int32_t)x.v[i] * f + (int64_t)(int32_t)y.v[i] * g;
+    const uint32_t k = ((uint32_t)t[0] * BN_PINV29) & M29;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t[i] += (int64_t)((uint64_t)k * kP29.v[i]);
+    Fq<6> r;
+    int64_t c = t[0] >> 29;
+#pragma unroll
+    for (int i = 1; i < 9; ++i) {
+        const int64_t s = t[i] + c + P3.v[i - 1];
+        r.v[i - 1] = (uint32_t)s & M29;
+        c = s >> 29;
+    }
+    r.v[8] = (uint32_t)(c + P3.v[8]);
+    return r;
+}
 template <int B>
-BN_INLINE Fq<2> fq_inv(const Fq<B>& a) { return fq_inv_w(a); }
+BN_INLINE Fq<2> fq_inv_bgcd(const Fq<B>& x) {
+    const Fq<1> y = fq_canonical(x);  // the plain integer x*R mod p
+    uint32_t a[9], b[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        a[i] = y.v[i];
+        b[i] = kP29.v[i];
+    }
+    Fq<2> u = fq_from_limbs<2>(Limbs9{{1, 0, 0, 0, 0, 0, 0, 0, 0}}), v = widen<2>(fq_zero());
+#pragma unroll 1
+    for (int round = 0; round < kInvRounds; ++round) {
+        // n = max(len(a), len(b), 60): the bit length of a | b
+        uint32_t n = 60;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            const uint32_t o = a[d] | b[d];
+            const uint32_t len = 29u * d + 32u - (uint32_t)__builtin_clz(o | 1u);
+            n = (o != 0 && len > n) ? len : n;
+        }
+        const uint32_t s = n - 31, dd = s / 29, off = s - 29 * dd;
+        uint32_t a0 = 0, a1 = 0, a2 = 0, b0 = 0, b1 = 0, b2 = 0;
+#pragma unroll
+        for (int d = 1; d < 9; ++d) {
+            const bool h = dd == (uint32_t)d;
+            a0 = h ? a[d] : a0;
+            b0 = h ? b[d] : b0;
+            a1 = h ? (d + 1 < 9 ? a[d + 1 < 9 ? d + 1 : 8] : 0u) : a1;
+            b1 = h ? (d + 1 < 9 ? b[d + 1 < 9 ? d + 1 : 8] : 0u) : b1;
+            a2 = h ? (d + 2 < 9 ? a[d + 2 < 9 ? d + 2 : 8] : 0u) : a2;
+            b2 = h ? (d + 2 < 9 ? b[d + 2 < 9 ? d + 2 : 8] : 0u) : b2;
+        }
+        const uint64_t wa = (uint64_t)a0 | ((uint64_t)a1 << 29) | ((uint64_t)a2 << 58);
+        const uint64_t wb = (uint64_t)b0 | ((uint64_t)b1 << 29) | ((uint64_t)b2 << 58);
+        uint64_t ab = (uint64_t)a[0] | (((wa >> off) & 0x7fffffffu) << 29);
+        uint64_t bb = (uint64_t)b[0] | (((wb >> off) & 0x7fffffffu) << 29);
+        int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll
+        for (int j = 0; j < 29; ++j) {
+            const bool odd = (ab & 1u) != 0;
+            const bool sw = odd && ab < bb;
+            const uint64_t ta = sw ? bb : ab, tb = sw ? ab : bb;
+            const int32_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+            ab = odd ? ta - tb : ta;
+            f0 = odd ? tf0 - tf1 : tf0;
+            g0 = odd ? tg0 - tg1 : tg0;
+            bb = tb;
+            f1 = tf1 + tf1;
+            g1 = tg1 + tg1;
+            ab >>= 1;
+        }
+        uint32_t na[9], nb[9];
+        const uint32_t ma = bgcd_lin_exact(a, b, f0, g0, na);
+        const uint32_t mb = bgcd_lin_exact(a, b, f1, g1, nb);
+        f0 = (int32_t)(((uint32_t)f0 ^ ma) - ma);
+        g0 = (int32_t)(((uint32_t)g0 ^ ma) - ma);
+        f1 = (int32_t)(((uint32_t)f1 ^ mb) - mb);
+        g1 = (int32_t)(((uint32_t)g1 ^ mb) - mb);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            a[i] = na[i];
+            b[i] = nb[i];
+        }
+        const Fq<2> nu = fq_fold(bgcd_lin_mont(u, v, f0, g0));
+        v = fq_fold(bgcd_lin_mont(u, v, f1, g1));
+        u = nu;
+    }
+#if defined(BN_HOST_CHECKS) && !defined(__HIP_DEVICE_COMPILE__)
+    // y != 0 must end with b == gcd == 1 (y == 0 keeps a = 0, b = p, v = 0 and
+    // returns 0, as the Fermat chain does)
+    uint32_t not_one = b[0] ^ 1u, nz = 0;
+    for (int i = 1; i < 9; ++i) not_one |= b[i];
+    for (int i = 0; i < 9; ++i) nz |= y.v[i];
+    if (nz && not_one) {
+        fprintf(stderr, "fq_inv_bgcd: %d rounds did not reach b == 1\n", kInvRounds);
+        abort();
+    }
+#endif
+    return fq_mul(v, fq_from_limbs<1>(kR3));
+}
+template <int B>
+BN_INLINE Fq<2> fq_inv(const Fq<B>& a) {
+#if BN_INV_BGCD
+    return fq_inv_bgcd(a);
+#else
+    return fq_inv_w(a);
+#endif
+}
 // x unchanged when its bound is <= L, else folded to 2 (decided at compile time)
 template <int L, int B>
 BN_INLINE auto pre(const Fq<B>& a) {
