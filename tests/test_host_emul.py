@@ -35,6 +35,19 @@ def test_fq_ops(rnd):
             assert O.mont_array_to_canon(H.call("he_fq_inv", X, out_words=8)) == [pow(v, -1, O.P)]
 
 
+def test_fq_inv_binary_gcd_sweep(rnd):
+    # fq_inv is the 19-round binary GCD (tower.h fq_inv_bgcd): random values,
+    # small values, powers of two, values next to p and to 2^254, 1 and p - 1;
+    # the host build aborts if a round count ever falls short (BN_HOST_CHECKS)
+    g = O.SplitMix64(77)
+    vals = rnd(600) + list(range(1, 40)) + [1 << k for k in range(254)] + [O.P - 1 - k for k in range(40)]
+    vals += [(1 << 253) + g.below(1 << 64) for _ in range(40)] + [O.P // 3, O.P // 2, (O.P + 1) // 2]
+    X = fe(vals).reshape(-1, 4)
+    for k, v in enumerate(vals):
+        assert O.mont_array_to_canon(H.call("he_fq_inv", X[k], out_words=8)) == [pow(v, -1, O.P)], v
+    assert O.mont_array_to_canon(H.call("he_fq_inv", fe([0]), out_words=8)) == [0]  # as the Fermat chain
+
+
 def test_fq_fold_value(rnd):
     # fold(64x + x - x + 20p-ish) == 64x + ... : compare with the exact residue
     for v in rnd(30) + [0, O.P - 1]:
