@@ -229,21 +229,22 @@ BN_INLINE Fq<2> fq_inv_bgcd(const Fq<B>& x) {
         const uint64_t wb = (uint64_t)b0 | ((uint64_t)b1 << 29) | ((uint64_t)b2 << 58);
         uint64_t ab = (uint64_t)a[0] | (((wa >> off) & 0x7fffffffu) << 29);
         uint64_t bb = (uint64_t)b[0] | (((wb >> off) & 0x7fffffffu) << 29);
-        int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+        // update factors packed as f + g*2^32 in one 64-bit word (the steps are
+        // linear, so the pack stays exact; |f|, |g| <= 2^29)
+        uint64_t pa = 1, pb = (uint64_t)1 << 32;  // (f0, g0) = (1, 0), (f1, g1) = (0, 1)
 #pragma unroll
         for (int j = 0; j < 29; ++j) {
             const bool odd = (ab & 1u) != 0;
-            const bool sw = odd && ab < bb;
-            const uint64_t ta = sw ? bb : ab, tb = sw ? ab : bb;
-            const int32_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
-            ab = odd ? ta - tb : ta;
-            f0 = odd ? tf0 - tf1 : tf0;
-            g0 = odd ? tg0 - tg1 : tg0;
+            const bool sw = odd & (ab < bb);
+            const uint64_t ta = sw ? bb : ab, tb = sw ? ab : bb, tp = sw ? pb : pa, tq = sw ? pa : pb;
+            ab = (ta - (odd ? tb : 0)) >> 1;
+            pa = tp - (odd ? tq : 0);
             bb = tb;
-            f1 = tf1 + tf1;
-            g1 = tg1 + tg1;
-            ab >>= 1;
+            pb = tq << 1;
         }
+        int32_t f0 = (int32_t)(uint32_t)pa, f1 = (int32_t)(uint32_t)pb;
+        int32_t g0 = (int32_t)((int64_t)(pa - (uint64_t)(int64_t)f0) >> 32);
+        int32_t g1 = (int32_t)((int64_t)(pb - (uint64_t)(int64_t)f1) >> 32);
         uint32_t na[9], nb[9];
         const uint32_t ma = bgcd_lin_exact(a, b, f0, g0, na);
         const uint32_t mb = bgcd_lin_exact(a, b, f1, g1, nb);
