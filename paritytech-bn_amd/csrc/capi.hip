@@ -62,6 +62,9 @@ constexpr int kFeSlots = 32;  // slot 0: Miller value, 1: easy-part result, 2..:
 // throughput path: 8192 pairs 3.58 vs 5.43 ms, 16384 pairs 6.05 vs 5.43 ms
 // (profiles/r2j_latency_sweep.jsonl).  BN254MI_FE_WIDE_MAX or bn_set_fe_wide_max override.
 constexpr size_t kFeWideMaxDefault = 8192;
+// batches up to this size run k_prepare_wide (8 lanes per pair: 2^14 pairs fill
+// the GPU at two waves per SIMD).  BN254MI_PREPARE_WIDE_MAX overrides (0: never).
+constexpr size_t kPrepareWideMaxDefault = 16384;
 
 size_t ws_bytes(size_t n) {
     return n * ((size_t)kCoeffFq * 9 * 4 + kPathLanes * (2 * 9 * 4 + 1) + (size_t)kFeSlots * kSlotWords * 4) + 64;
@@ -238,10 +241,22 @@ int stage(bn_ctx* c, size_t bytes) {
 }
 hipStream_t pick(bn_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
+// to_affine + the 87 line coefficients of m pairs into c->coeffs / paff / flags:
+// eight lanes per pair (k_prepare_wide, about a third of the step latency) while
+// the batch leaves the GPU underfilled, two lanes per pair (k_prepare) otherwise
+static int prepare(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int mode, hipStream_t s) {
+    if (m <= c->prepare_wide_max)
+        k_prepare_wide<<<grid_for(kPrepareWideLanes * m), kBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags,
+                                                                          c->d_err, mode);
+    else
+        k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags, c->d_err, mode);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+
 // Miller values of n pairs into slot 0 (lane-strided, stride = n); n <= c->cap
 int miller_values(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int mode, hipStream_t s) {
-    k_prepare<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(d_p, d_q, n, c->coeffs, c->paff, c->flags, c->d_err, mode);
-    HIPCHK(c, hipGetLastError());
+    RET_IF(prepare(c, d_p, d_q, n, mode, s));
     k_miller<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, n, c->slots);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
@@ -337,8 +352,7 @@ SegPlan seg_plan(size_t n) {
 // S * nchunks) of `parts`
 int chunk_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int mode, const SegPlan& plan,
                   uint32_t* parts, size_t nchunks, size_t k, hipStream_t s) {
-    k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags, c->d_err, mode);
-    HIPCHK(c, hipGetLastError());
+    RET_IF(prepare(c, d_p, d_q, m, mode, s));
     k_miller_seg<<<grid_for(kPathLanes * plan.S * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
                                                                        slot_region(c, kRegionSeg));
     HIPCHK(c, hipGetLastError());
@@ -478,6 +492,8 @@ int bn_ctx_create(int device, bn_ctx** out) {
     c->fe_wide_max = kFeWideMaxDefault;
     if (const char* e = getenv("BN254MI_FE_WIDE_MAX")) c->fe_wide_max = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("BN254MI_MILLER_FORM")) c->miller_form = atoi(e);
+    c->prepare_wide_max = kPrepareWideMaxDefault;
+    if (const char* e = getenv("BN254MI_PREPARE_WIDE_MAX")) c->prepare_wide_max = (size_t)strtoull(e, nullptr, 10);
     Prog P;
     c->fe_out = (int)build_final_exp(P);
     P.finalize({(uint32_t)c->fe_out});
@@ -562,8 +578,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             // latency path: the Miller loop in segments on 2 * S lanes per pairing,
             // recombined and exponentiated on a 16-lane group per pairing
             const SegPlan plan = seg_plan(m);
-            k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags,
-                                                                  c->d_err, 0);
+            RET_IF(prepare(c, d_p + off, d_q + off, m, 0, s));
             mark(1);
             k_miller_seg<<<grid_for(kPathLanes * plan.S * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
                                                                                slot_region(c, kRegionSeg));
@@ -854,8 +869,7 @@ int bn_g2_precompute_many(bn_ctx* c, const bn_g2* q, size_t n, bn_fq2* out) {
         std::vector<bn_g1> ones(m, one);
         HIPCHK(c, hipMemcpyAsync(dp, ones.data(), m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
-        k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(dp, dq, m, c->coeffs, c->paff, c->flags,
-                                                                       c->d_err, 1);
+        RET_IF(prepare(c, dp, dq, m, 1, c->stream));
         k_coeffs_store<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(c->coeffs, m, dout);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(out + off * BN_NUM_COEFFS * 3, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));

@@ -36,6 +36,8 @@ struct bn_ctx {
     // coefficient traffic); 0 = k_prepare (line coefficients to HBM) + k_miller;
     // 2 = k_prepare + k_miller_seg with one segment
     int miller_form = 1;
+    // batches of at most this many pairs take k_prepare_wide (8 lanes per pair)
+    size_t prepare_wide_max = 0;
     int* d_err = nullptr;
     // staging for host-buffer calls (device)
     size_t stage_bytes = 0;

@@ -446,8 +446,16 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
 __global__ void __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
                           uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
                           int* __restrict__ err, int mode);
+// the same outputs on kPrepareWideLanes lanes per pair (kernels_pairing.hip): four
+// lane pairs run each line step's independent products side by side
+constexpr int kPrepareWideLanes = 8;
+__global__ void __launch_bounds__(kBlock) k_prepare_wide(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
+                                                         size_t n, uint32_t* __restrict__ coeffs,
+                                                         uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
+                                                         int* __restrict__ err, int mode);
 __global__ void __launch_bounds__(kBlock) k_coeffs_store(const uint32_t* __restrict__ coeffs, size_t n,
-                                                         bn_fq2* __restrict__ out);__global__ void __launch_bounds__(kBlock) k_pairing_fused(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
+                                                         bn_fq2* __restrict__ out);
+__global__ void __launch_bounds__(kBlock) k_pairing_fused(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
                                                           size_t n, uint8_t* __restrict__ flags, int* __restrict__ err,
                                                           int mode, uint32_t* __restrict__ f_out);
 __global__ void __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ coeffs, const uint32_t* __restrict__ paff,

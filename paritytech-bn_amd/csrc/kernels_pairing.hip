@@ -7,6 +7,8 @@
 #ifndef BN_FOLD_LDS
 #define BN_FOLD_LDS 1
 #endif
+#include <type_traits>
+
 #include "fq.h"
 #define BN_SPLIT BN_PATH_SPLIT
 #include "kernels.h"
@@ -90,6 +92,149 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare(const bn_g1* __
         st_fq2(coeffs, nl, l, k * 6 + 4, e.ell_vv);
     });
 }
+
+#if BN_SPLIT
+// ---------------------------------------------------------------- k_prepare_wide
+// The same to_affine + 87 line coefficients for small batches, on EIGHT lanes
+// per pair: four lane pairs ("slots") run each line step's independent Fq2
+// products side by side -- the doubling step's ten products in three layers,
+// the mixed addition's fourteen in four -- and exchange the results over
+// ds_bpermute; the sums, halvings and narrowings between layers run on every
+// slot alike.  A lone pair's 87 dependent steps are the latency of k_prepare
+// (DESIGN.md §5); here each step issues about a third of the instructions per
+// lane.  Same formulas (fq2_mul(x, x) for the squares: the same residues), so the
+// coefficients are the same values; slot 0 stores them, in k_prepare's layout.
+constexpr int kPW = kPrepareWideLanes;  // lanes per pair (kernels.h)
+__device__ __forceinline__ int pw_slot() { return (int)((__lane_id() >> 1) & 3u); }
+// this lane's coordinate of x as computed by slot j of its group
+template <int B>
+__device__ __forceinline__ Fq2<B> pw_from(const Fq2<B>& x, int j) {
+    const int src = (int)((__lane_id() & ~7u) | ((unsigned)j << 1) | (__lane_id() & 1u));
+    Fq2<B> r;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) r.c.v[d] = (uint32_t)__shfl((int)x.c.v[d], src);
+    return r;
+}
+template <int B>
+__device__ __forceinline__ Fq2<B> pw_pick(int k, const Fq2<B>& a0, const Fq2<B>& a1, const Fq2<B>& a2,
+                                          const Fq2<B>& a3) {
+    return fq2_select(k == 0, a0, fq2_select(k == 1, a1, fq2_select(k == 2, a2, a3)));
+}
+template <class T>
+struct Fq2K;
+template <int B>
+struct Fq2K<Fq2<B>> {
+    static constexpr int K = B;
+};
+// one layer: slot k computes x_k * y_k (each operand folded to bound <= 40 as
+// fq2_mul would, then all joined to one static bound so the slots run one stream)
+template <class X0, class Y0, class X1, class Y1, class X2, class Y2, class X3, class Y3>
+__device__ __forceinline__ auto pw_mul(int k, const X0& x0_in, const Y0& y0_in, const X1& x1_in, const Y1& y1_in,
+                                       const X2& x2_in, const Y2& y2_in, const X3& x3_in, const Y3& y3_in) {
+    const auto x0 = pre<40>(x0_in);
+    const auto y0 = pre<40>(y0_in);
+    const auto x1 = pre<40>(x1_in);
+    const auto y1 = pre<40>(y1_in);
+    const auto x2 = pre<40>(x2_in);
+    const auto y2 = pre<40>(y2_in);
+    const auto x3 = pre<40>(x3_in);
+    const auto y3 = pre<40>(y3_in);
+    constexpr int JX = kjoin(kjoin(Fq2K<std::decay_t<decltype(x0)>>::K, Fq2K<std::decay_t<decltype(x1)>>::K),
+                             kjoin(Fq2K<std::decay_t<decltype(x2)>>::K, Fq2K<std::decay_t<decltype(x3)>>::K));
+    constexpr int JY = kjoin(kjoin(Fq2K<std::decay_t<decltype(y0)>>::K, Fq2K<std::decay_t<decltype(y1)>>::K),
+                             kjoin(Fq2K<std::decay_t<decltype(y2)>>::K, Fq2K<std::decay_t<decltype(y3)>>::K));
+    return fq2_mul(pw_pick(k, widen<JX>(x0), widen<JX>(x1), widen<JX>(x2), widen<JX>(x3)),
+                   pw_pick(k, widen<JY>(y0), widen<JY>(y1), widen<JY>(y2), widen<JY>(y3)));
+}
+// doubling_step (curve.h) in three layers
+__device__ __forceinline__ Ell pw_doubling_step(G2Proj& s, int k) {
+    const auto l1 = pw_mul(k, s.x, s.y, s.y, s.y, s.z, s.z, s.x, s.x);  // x*y, y^2, z^2, x^2
+    const auto a = fq2_half(pw_from(l1, 0));
+    const auto b = pw_from(l1, 1);
+    const auto c = pw_from(l1, 2);
+    const auto j = pw_from(l1, 3);
+    const auto d = fq2_add(fq2_add(c, c), c);
+    const auto yz = fq2_add(s.y, s.z);
+    const auto bc = g2_coeff_b();
+    const auto l2 = pw_mul(k, bc, d, yz, yz, bc, d, yz, yz);  // e = b' * 3c, (y + z)^2
+    const auto e = pw_from(l2, 0);
+    const auto h = fq2_sub(pw_from(l2, 1), fq2_add(b, c));
+    const auto f = fq2_add(fq2_add(e, e), e);
+    const auto g = fq2_half(fq2_add(b, f));
+    const auto i = fq2_sub(e, b);
+    const auto l3 = pw_mul(k, a, fq2_sub(b, f), g, g, e, e, b, h);  // x', g^2, e^2, z'
+    const auto e_sq = pw_from(l3, 2);
+    s.x = narrow<kPt>(pw_from(l3, 0));
+    s.y = narrow<kPt>(fq2_sub(pw_from(l3, 1), fq2_add(fq2_add(e_sq, e_sq), e_sq)));
+    s.z = narrow<kPt>(pw_from(l3, 3));
+    return {narrow<kLine>(fq2_mul_xi(i)), narrow<kLine>(fq2_neg(h)), narrow<kLine>(fq2_add(fq2_add(j, j), j))};
+}
+// mixed_addition_step (curve.h) in four layers
+template <int BB>
+__device__ __forceinline__ Ell pw_mixed_addition_step(G2Proj& s, const G2Aff<BB>& base, int k) {
+    const auto l1 = pw_mul(k, s.z, base.x, s.z, base.y, s.z, base.x, s.z, base.y);  // z*bx, z*by
+    const auto d = fq2_sub(s.x, pw_from(l1, 0));
+    const auto e = fq2_sub(s.y, pw_from(l1, 1));
+    const auto l2 = pw_mul(k, d, d, e, e, e, base.x, d, base.y);  // f = d^2, g = e^2, e*bx, d*by
+    const auto f = pw_from(l2, 0);
+    const auto g = pw_from(l2, 1);
+    const auto l0 = fq2_mul_xi(fq2_sub(pw_from(l2, 2), pw_from(l2, 3)));
+    const auto l3 = pw_mul(k, d, f, s.x, f, s.z, g, s.z, g);  // h = d*f, i = x*f, z*g
+    const auto h = pw_from(l3, 0);
+    const auto i = pw_from(l3, 1);
+    const auto jj = fq2_sub(fq2_add(pw_from(l3, 2), h), fq2_add(i, i));
+    const auto l4 = pw_mul(k, d, jj, e, fq2_sub(i, jj), h, s.y, s.z, h);  // nx, e*(i - j), h*y, nz
+    s.x = narrow<kPt>(pw_from(l4, 0));
+    s.y = narrow<kPt>(fq2_sub(pw_from(l4, 1), pw_from(l4, 2)));
+    s.z = narrow<kPt>(pw_from(l4, 3));
+    return {narrow<kLine>(l0), narrow<kLine>(d), narrow<kLine>(fq2_neg(e))};
+}
+
+__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare_wide(const bn_g1* __restrict__ p,
+                                                                     const bn_g2* __restrict__ q, size_t n,
+                                                                     uint32_t* __restrict__ coeffs,
+                                                                     uint32_t* __restrict__ paff,
+                                                                     uint8_t* __restrict__ flags,
+                                                                     int* __restrict__ err, int mode) {
+    fold_table_init();
+    const size_t l = lane_id(), i = l / kPW, nl = kL * n;
+    if (i >= n) return;
+    const size_t lt = i * kL + (l & 1);  // this lane's index in k_prepare's per-pair arrays
+    const int k = pw_slot();
+    const bool st = k == 0;
+    const PairAffine a = pair_to_affine(p, q, i, lt, flags, err, st ? mode : 0);
+    if (st) {
+        st_fq(paff, nl, lt, 0, a.px);
+        st_fq(paff, nl, lt, 1, a.py);
+    }
+    auto emit = [&](int c, const Ell& e) {
+        if (st) {
+            st_fq2(coeffs, nl, lt, c * 6 + 0, e.ell_0);
+            st_fq2(coeffs, nl, lt, c * 6 + 2, e.ell_vw);
+            st_fq2(coeffs, nl, lt, c * 6 + 4, e.ell_vv);
+        }
+    };
+    // g2_precompute (pairing.h), AffineG2::precompute mod.rs:701-727
+    const G2Aff<kPt>& qa = a.qa;
+    G2Proj r = {qa.x, qa.y, widen<kPt>(fq2_one())};
+    const auto qy_neg = fq2_neg(qa.y);
+    int c = 0;
+#pragma unroll 1
+    for (int d = 0; d < BN_NAF_DIGITS; ++d) {
+        emit(c++, pw_doubling_step(r, k));
+        if ((kNafNonzero >> d) & 1u) {
+            const bool minus = (kNafMinus >> d) & 1u;
+            const G2Aff<kPt> base = {qa.x, fq2_select(minus, widen<kPt>(qy_neg), qa.y)};
+            emit(c++, pw_mixed_addition_step(r, base, k));
+        }
+    }
+    G2Aff<kPt> q1 = mul_by_q(qa);
+    G2Aff<kPt> q2 = mul_by_q(q1);
+    q2.y = narrow<kPt>(fq2_neg(q2.y));
+    emit(c++, pw_mixed_addition_step(r, q1, k));
+    emit(c++, pw_mixed_addition_step(r, q2, k));
+}
+#endif
 
 // The coefficients k_prepare wrote for pair i -> the reference images of its
 // G2Precomp (mod.rs:566-577): 87 x {ell_0, ell_vw, ell_vv}, each a canonical Fq2
