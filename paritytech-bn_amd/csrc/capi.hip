@@ -325,7 +325,10 @@ constexpr int kRegionSeg = 8;  // k_miller_seg output: S * n elements from regio
 SegPlan seg_plan(size_t n) {
     SegPlan p{};
     int S = 1;
-    while (S < kMaxSeg && (size_t)S * n < ((size_t)1 << 16)) S *= 2;
+    // S doubles while S*n lane pairs leave the GPU underfilled; 16 segments only
+    // for the smallest batches (profiles/r2ac_latency_seg16.txt: 16 helps up to
+    // ~1024 pairs, costs at 4096 through the longer Horner recombination)
+    while (S < kMaxSeg && (size_t)S * n < ((size_t)1 << 16) && !(S >= 8 && (size_t)S * n >= ((size_t)1 << 14))) S *= 2;
     p.S = S;
     auto cost = [](int d) { return 36 + 39 + (((kNafNonzero >> d) & 1u) ? 39 : 0); };
     int total = 2 * 39;

@@ -427,7 +427,7 @@ inline void vm_step(uint32_t out[2], uint32_t op, uint32_t d, uint32_t a, uint32
 
 // Segments of the Miller loop's 64 NAF digits (k_miller_seg / k_horner_wide):
 // segment s covers digits [lo[s], hi[s]) and starts at line coefficient idx[s]
-constexpr int kMaxSeg = 8;
+constexpr int kMaxSeg = 16;
 struct SegPlan {
     int S;
     int lo[kMaxSeg], hi[kMaxSeg], idx[kMaxSeg];
