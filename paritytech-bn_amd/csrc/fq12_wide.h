@@ -138,14 +138,15 @@ __device__ __noinline__ Fq<2> w12_cyc(Fq<2> a) {
     const Fq<2> x0 = w_get<2>(A_, 2 * k), x1 = w_get<2>(A_, 2 * k + 1);
     const Fq<2> y0 = w_get<2>(A_, 2 * k + 6), y1 = w_get<2>(A_, 2 * k + 7);
     const Fq<2> xy0 = w_get<2>(X_, 2 * k + 6), xy1 = w_get<2>(X_, 2 * k + 7);  // xi * y
-    // U = hi ? x + y : x,  V = hi ? xi*y + x : y
+    // U = hi ? x + y : x,  V = hi ? xi*y + x : y (V's digits stay lazy: the column
+    // budget of u*vo + u*vx is 1*2 + 1*4 with U normalized)
     const Fq<4> u0 = fq_norm(fq_pick(hi, fq_add(x0, y0), x0));
     const Fq<4> u1 = fq_norm(fq_pick(hi, fq_add(x1, y1), x1));
-    const Fq<4> v0 = fq_norm(fq_pick(hi, fq_add(xy0, x0), y0));
-    const Fq<4> v1 = fq_norm(fq_pick(hi, fq_add(xy1, x1), y1));
+    const auto v0 = fq_pick(hi, fq_add(xy0, x0), y0);
+    const auto v1 = fq_pick(hi, fq_add(xy1, x1), y1);
     // lane c of U*V: c0 = u0 v0 - u1 v1, c1 = u0 v1 + u1 v0
-    const Fq<4> vo = fq_select(w.c != 0, v1, v0);
-    const Fq<4> vx = fq_select(w.c != 0, v0, fq_neg(v1));
+    const auto vo = fq_select(w.c != 0, v1, v0);
+    const auto vx = fq_pick(w.c != 0, v0, fq_neg_lazy(v1));
     const auto p = fq_dot2(u0, vo, u1, vx);
     const Fq<2> pn = w_narrow(p);
     w_put(P_, w.l, pn);
@@ -157,11 +158,13 @@ __device__ __noinline__ Fq<2> w12_cyc(Fq<2> a) {
     const Fq<2> pu = w_get<2>(P_, 2 * (ka + 3) + w.c), pv = w_get<2>(P_, 2 * ka + w.c);
     const Fq<2> pw = w_get<2>(Q_, 2 * ka + w.c);
     const Fq<2> px = w.e == 1 ? w_get<2>(Q_, 4 + w.c) : w_get<2>(P_, (w.e >= 3 ? w.e - 3 : 0) + w.c);
+    // one stream for both parities: 3*T + (-2a | 2a), T = ta (even e) or 2*px (odd e)
+    const bool even = (w.e & 1) == 0;
     const auto ta = fq_norm(fq_sub(fq_sub(pu, pv), pw));
-    const Fq<2> oa = fq_fold(fq_sub(fq_add(ta, fq_add(ta, ta)), fq_dbl(a)));
-    const auto tb = fq_dbl(px);
-    const Fq<2> ob = fq_fold(fq_add(fq_add(tb, fq_add(tb, tb)), fq_dbl(a)));
-    return fq_select((w.e & 1) == 0, oa, ob);
+    const auto t = fq_pick(even, ta, fq_dbl(px));
+    const auto a2 = fq_dbl(a);
+    const auto s = fq_pick(even, fq_neg_lazy(a2), a2);
+    return fq_fold(fq_add(fq_add(t, fq_add(t, t)), s));
 }
 
 // unitary inverse (fq12.rs:126-128): the w^odd coefficients negate
