@@ -41,11 +41,79 @@ BN_INLINE void g2_precompute(const G2Aff<B>& q, Emit&& emit) {
     emit(k++, mixed_addition_step(r, q2));
 }
 
+#if BN_SPLIT
+// The same product f * (x0 + x4 w^3 + x2 w^4) on the two-lane layout, as six
+// column sums reduced once each.  In the w-basis (f_m = coefficient of w^m:
+// c0.c(m/2) for even m, c1.c((m-1)/2) for odd m; w^6 = xi)
+//   out_m = f_m x0 + f_(m-3) x4 + f_(m-4) x2,  indices mod 6, times xi on a wrap,
+// with xi moved onto the f side (xi f_2 .. xi f_5).  Each lane sums its
+// coordinate of three Fq2 products -- six digit products, own(u) * v0 +
+// partner(u) * (lane 0: K*p - v1, lane 1: v1) -- in one column accumulator and
+// reduces once: 36 products + 6 reductions per lane instead of the 13-product
+// formula's 26 + 13, and no combining adds, subtractions or folds.  The line
+// side's operand forms are built once per coefficient.  The value is the
+// reference's product (fq12.rs:130-196) -- the same residues.  BN_LINE_LAZY = 0
+// keeps the 13-product formula (A/B).
+struct LineOps {
+    Fq<kLine> y;  // v0 on both lanes
+    Fq<8> w;      // lane 0: K*p - v1, lane 1: v1 (normalized digits, value <= (kLine + 1) p)
+};
+template <int X>
+BN_INLINE LineOps line_ops(const Fq2<X>& v_in) {
+    const Fq<kv(X)> v = fq_norm(v_in.c);
+    const Fq<kv(X)> pv = fq_partner(v);
+    const bool odd = lane_odd();
+    return {widen<kLine>(fq_select(odd, pv, v)), widen<8>(fq_norm(fq_pick(odd, v, fq_neg_lazy(pv))))};
+}
+// t += u * v for this lane's coordinate (u: f side, normalized)
+BN_INLINE void acc_mad2(Acc& t, const Fq<2>& u, const LineOps& v) {
+    acc_mad(t, u, v.y);
+    acc_mad(t, fq_partner(u), v.w);
+}
+template <int F, int X>
+BN_INLINE Fq12<2> fq12_mul_by_024_lazy(const Fq12<F>& f_in, const Fq2<X>& x0_in, const Fq2<X>& x4_in,
+                                       const Fq2<X>& x2_in) {
+    static_assert(kl(F) == 1 && kv(F) <= 2, "fq12_mul_by_024_lazy: f normalized, bound 2");
+    const LineOps x0 = line_ops(x0_in), x4 = line_ops(x4_in), x2 = line_ops(x2_in);
+    const Fq<2> f0 = widen<2>(f_in.c0.c0.c), f1 = widen<2>(f_in.c1.c0.c), f2 = widen<2>(f_in.c0.c1.c);
+    const Fq<2> f3 = widen<2>(f_in.c1.c1.c), f4 = widen<2>(f_in.c0.c2.c), f5 = widen<2>(f_in.c1.c2.c);
+    auto xi = [](const Fq<2>& u) { return fq2_fold(fq2_mul_xi(Fq2<2>{u})).c; };
+    const Fq<2> g2 = xi(f2), g3 = xi(f3), g4 = xi(f4), g5 = xi(f5);
+    // value per lane <= 3 * (2p * 4p + 2p * 5p) = 54 p^2: the reduction is below 1.4 p
+    auto out = [&](const Fq<2>& a, const LineOps& va, const Fq<2>& b, const LineOps& vb, const Fq<2>& c,
+                   const LineOps& vc) {
+        Acc t = {};
+        acc_mad2(t, a, va);
+        acc_mad2(t, b, vb);
+        acc_mad2(t, c, vc);
+        return Fq2<2>{acc_redc<2>(t)};
+    };
+    // (computing the outputs last-first with each xi*f_k made just before its first
+    // use spills less -- 352 vs 392 B per lane -- but ran 2-3 % slower:
+    // profiles/r2ai_ab_line_lazy.txt)
+    const Fq2<2> o0 = out(f0, x0, g3, x4, g2, x2);
+    const Fq2<2> o1 = out(f1, x0, g4, x4, g3, x2);
+    const Fq2<2> o2 = out(f2, x0, g5, x4, g4, x2);
+    const Fq2<2> o3 = out(f3, x0, f0, x4, g5, x2);
+    const Fq2<2> o4 = out(f4, x0, f1, x4, f0, x2);
+    const Fq2<2> o5 = out(f5, x0, f2, x4, f1, x2);
+    return {{o0, o2, o4}, {o1, o3, o5}};
+}
+#endif
+
+#ifndef BN_LINE_LAZY
+#define BN_LINE_LAZY 1
+#endif
 // f <- f * line(P): ell_vw.scale(Py), ell_vv.scale(Px)  (mod.rs:589)
 template <int B, int PB>
 BN_INLINE Fq12<kF> apply_line(const Fq12<B>& f, const Ell& c, const Fq<PB>& px, const Fq<PB>& py) {
+#if BN_SPLIT && BN_LINE_LAZY
+    return widen<kF>(fq12_mul_by_024_lazy(narrow12<2>(f), c.ell_0, narrow<kLine>(fq2_scale(c.ell_vw, py)),
+                                          narrow<kLine>(fq2_scale(c.ell_vv, px))));
+#else
     return narrow12<kF>(fq12_mul_by_024(f, c.ell_0, narrow<kLine>(fq2_scale(c.ell_vw, py)),
                                         narrow<kLine>(fq2_scale(c.ell_vv, px))));
+#endif
 }
 
 // G2Precomp::miller_loop, mod.rs:579-607.  `line(k)` returns coefficient k.
