@@ -9,6 +9,7 @@
 #include <initializer_list>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels.h"
@@ -240,6 +241,40 @@ int stage(bn_ctx* c, size_t bytes) {
     return BN_OK;
 }
 hipStream_t pick(bn_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
+
+// ---------------------------------------------------------------- host pipeline helpers
+constexpr size_t kHostPiece = size_t(1) << 16;  // pairs per piece of bn_pairing_many's host pipeline
+size_t round256(size_t b) { return (b + 255) & ~(size_t)255; }
+// pinned bounce buffers of bn_pairing_many (grown, never shrunk); the caller
+// has drained the copy streams, which are the buffers' only device users
+int pin_reserve(bn_ctx* c, size_t bytes) {
+    if (bytes <= c->pin_bytes) return BN_OK;
+    if (c->pin) HIPCHK(c, hipHostFree(c->pin));
+    c->pin = nullptr;
+    c->pin_bytes = 0;
+    HIPCHK(c, hipHostMalloc(&c->pin, bytes, hipHostMallocDefault));
+    c->pin_bytes = bytes;
+    return BN_OK;
+}
+// memcpy split over up to 8 host threads for large copies (a single thread
+// moves ~10 GB/s, a 2^16-pair piece is 44 MB)
+void par_copy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPerThread = size_t(4) << 20;
+    const size_t nt = std::min<size_t>(8, bytes / kPerThread);
+    if (nt <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t per = ((bytes + nt - 1) / nt + 63) & ~(size_t)63;
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) {
+        const size_t lo = t * per;
+        if (lo >= bytes) break;
+        th.emplace_back([=] { memcpy((uint8_t*)dst + lo, (const uint8_t*)src + lo, std::min(per, bytes - lo)); });
+    }
+    memcpy(dst, src, std::min(per, bytes));
+    for (auto& t : th) t.join();
+}
 
 // to_affine + the 87 line coefficients of m pairs into c->coeffs / paff / flags:
 // eight lanes per pair (k_prepare_wide, about a third of the step latency) while
@@ -495,6 +530,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
     c->fe_wide_max = kFeWideMaxDefault;
     if (const char* e = getenv("BN254MI_FE_WIDE_MAX")) c->fe_wide_max = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("BN254MI_MILLER_FORM")) c->miller_form = atoi(e);
+    if (const char* e = getenv("BN254MI_HOST_PIPELINE")) c->host_pipeline = atoi(e);
     c->prepare_wide_max = kPrepareWideMaxDefault;
     if (const char* e = getenv("BN254MI_PREPARE_WIDE_MAX")) c->prepare_wide_max = (size_t)strtoull(e, nullptr, 10);
     Prog P;
@@ -505,7 +541,14 @@ int bn_ctx_create(int device, bn_ctx** out) {
         delete c;
         return BN_ERR_INVALID_ARGUMENT;
     }
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    bool events_ok = true;
+    if (hipSetDevice(device) == hipSuccess)
+        for (hipEvent_t* e : {&c->ev_in[0], &c->ev_in[1], &c->ev_comp[0], &c->ev_comp[1], &c->ev_out[0], &c->ev_out[1]})
+            events_ok = events_ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    if (!events_ok || hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->h2d, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess ||
         hipMalloc(&c->d_prog, P.s.size() * 4) != hipSuccess ||
@@ -523,7 +566,14 @@ int bn_ctx_destroy(bn_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->ws_pending) (void)hipEventSynchronize(c->ws_event);
     (void)hipStreamSynchronize(c->stream);
+    for (hipStream_t s : {c->h2d, c->d2h})
+        if (s) (void)hipStreamSynchronize(s);
     if (c->ws_event) (void)hipEventDestroy(c->ws_event);
+    for (hipEvent_t e : {c->ev_in[0], c->ev_in[1], c->ev_comp[0], c->ev_comp[1], c->ev_out[0], c->ev_out[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (c->pin) (void)hipHostFree(c->pin);
+    for (hipStream_t s : {c->h2d, c->d2h})
+        if (s) (void)hipStreamDestroy(s);
     for (void* p : {(void*)c->coeffs, (void*)c->paff, (void*)c->slots, (void*)c->flags, (void*)c->d_err,
                     (void*)c->d_prog, c->stage})
         if (p) (void)hipFree(p);
@@ -660,11 +710,62 @@ int bn_get_phase_times(bn_ctx* c, float* ms, int* launches) {
     return BN_OK;
 }
 
-int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
-    if (c && !c->subs.empty()) return bn_multi_pairing_many(c, p, q, n, out);
-    CTX_GUARD_HOST(c);  // held for the whole call: staging, kernels, readback
-    if (n == 0) return BN_OK;
-    if (!p || !q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+// bn_pairing_many on host buffers: pieces of up to kHostPiece pairs flow
+// through two pinned bounce buffers and two device staging halves.  Piece k's
+// inputs are copied by host threads into pinned half k&1, DMA'd on the h2d
+// stream, computed on the context stream and DMA'd back on the d2h stream,
+// while the host copies piece k+1 in and piece k-1 out (A/B against pageable
+// hipMemcpyAsync of the caller's buffers: DESIGN.md §8).  The caller's lock is
+// held throughout.
+static int pairing_many_host(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
+    const size_t piece = n < kHostPiece ? n : kHostPiece;
+    const size_t o_q = round256(piece * sizeof(bn_g1));
+    const size_t o_out = o_q + round256(piece * sizeof(bn_g2));
+    const size_t half = o_out + round256(piece * sizeof(bn_gt));
+    RET_IF(stage(c, 2 * half));
+    RET_IF(pin_reserve(c, 2 * half));
+    RET_IF(clear_err(c, c->stream));
+    // the copy streams start after the workspace's previous users (CTX_GUARD_HOST
+    // ordered c->stream after them); ev_comp doubles as "stage half free"
+    for (int b = 0; b < 2; ++b) HIPCHK(c, hipEventRecord(c->ev_comp[b], c->stream));
+    const size_t np = (n + piece - 1) / piece;
+    auto rows = [&](size_t k) { return std::min(piece, n - k * piece); };
+    auto drain = [&](size_t k) -> int {  // piece k's results: pinned -> caller
+        const int b = (int)(k & 1);
+        HIPCHK(c, hipEventSynchronize(c->ev_out[b]));
+        par_copy(out + k * piece, (uint8_t*)c->pin + b * half + o_out, rows(k) * sizeof(bn_gt));
+        return BN_OK;
+    };
+    for (size_t k = 0; k < np; ++k) {
+        const int b = (int)(k & 1);
+        const size_t off = k * piece, m = rows(k);
+        if (k >= 2) RET_IF(drain(k - 2));  // frees pinned half b (and its D2H source)
+        uint8_t* hp = (uint8_t*)c->pin + b * half;
+        uint8_t* dp = (uint8_t*)c->stage + b * half;
+        par_copy(hp, p + off, m * sizeof(bn_g1));
+        par_copy(hp + o_q, q + off, m * sizeof(bn_g2));
+        HIPCHK(c, hipStreamWaitEvent(c->h2d, c->ev_comp[b], 0));  // piece k-2 has read stage half b
+        HIPCHK(c, hipMemcpyAsync(dp, hp, m * sizeof(bn_g1), hipMemcpyHostToDevice, c->h2d));
+        HIPCHK(c, hipMemcpyAsync(dp + o_q, hp + o_q, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->h2d));
+        HIPCHK(c, hipEventRecord(c->ev_in[b], c->h2d));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_in[b], 0));
+        RET_IF(pairing_many_dev_impl(c, (const bn_g1*)dp, (const bn_g2*)(dp + o_q), m, (bn_gt*)(dp + o_out),
+                                     c->stream));
+        HIPCHK(c, hipEventRecord(c->ev_comp[b], c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->d2h, c->ev_comp[b], 0));
+        HIPCHK(c, hipMemcpyAsync(hp + o_out, dp + o_out, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->d2h));
+        HIPCHK(c, hipEventRecord(c->ev_out[b], c->d2h));
+    }
+    for (size_t k = np >= 2 ? np - 2 : 0; k < np; ++k) RET_IF(drain(k));
+    int bits = 0;
+    RET_IF(check_err(c, c->stream, &bits));
+    if (bits & (1 << BN_ERR_FE_ZERO)) return fail(c, BN_ERR_FE_ZERO, "miller loop cannot produce zero");
+    return BN_OK;
+}
+
+// the A/B form ($BN254MI_HOST_PIPELINE=0): hipMemcpyAsync straight from and to
+// the caller's (pageable) buffers, one chunk at a time on the context stream
+static int pairing_many_pageable(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
     for (size_t off = 0; off < n; off += kChunk) {
         const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
         RET_IF(stage(c, m * (sizeof(bn_g1) + sizeof(bn_g2) + sizeof(bn_gt))));
@@ -681,6 +782,24 @@ int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* 
         if (bits & (1 << BN_ERR_FE_ZERO)) return fail(c, BN_ERR_FE_ZERO, "miller loop cannot produce zero");
     }
     return BN_OK;
+}
+
+int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
+    if (c && !c->subs.empty()) return bn_multi_pairing_many(c, p, q, n, out);
+    CTX_GUARD_HOST(c);  // held for the whole call: staging, kernels, readback
+    if (n == 0) return BN_OK;
+    if (!p || !q || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    // one piece has nothing to overlap, and the runtime's own pageable copies
+    // measured ~6 % faster there (12.0 vs 12.6 ms at 2^16 pairs); the pipeline
+    // wins from two pieces on (2^20: 171 vs 191-199 ms; profiles/r2ak_host_e2e_ab.jsonl)
+    const bool pipe = c->host_pipeline == 2 || (c->host_pipeline == 1 && n > kHostPiece);
+    const int rc = pipe ? pairing_many_host(c, p, q, n, out) : pairing_many_pageable(c, p, q, n, out);
+    // an early error may leave copies queued: nothing may still touch the pinned
+    // or staging buffers when the call returns
+    (void)hipStreamSynchronize(c->h2d);
+    (void)hipStreamSynchronize(c->d2h);
+    (void)hipStreamSynchronize(c->stream);
+    return rc;
 }
 
 // The Miller product of n host pairs -> *out (host image), then pairing_batch's

@@ -42,6 +42,15 @@ struct bn_ctx {
     // staging for host-buffer calls (device)
     size_t stage_bytes = 0;
     void* stage = nullptr;
+    // bn_pairing_many's host pipeline (capi.hip): two pinned bounce buffers, the
+    // copy streams and the per-buffer events (created with the context);
+    // $BN254MI_HOST_PIPELINE: 1 (default) pipeline above one piece, 0 never
+    // (pageable A/B form), 2 always
+    int host_pipeline = 1;
+    size_t pin_bytes = 0;
+    void* pin = nullptr;
+    hipStream_t h2d = nullptr, d2h = nullptr;
+    hipEvent_t ev_in[2] = {}, ev_comp[2] = {}, ev_out[2] = {};
     // The workspace (coeffs, paff, slots, flags, d_err, stage) is shared by every
     // call on this context.  Host-side, the mutex serializes the calls; device-side,
     // every workspace user records ws_event on its stream when it has enqueued its
