@@ -243,7 +243,13 @@ int stage(bn_ctx* c, size_t bytes) {
 hipStream_t pick(bn_ctx* c, void* s) { return s ? (hipStream_t)s : c->stream; }
 
 // ---------------------------------------------------------------- host pipeline helpers
-constexpr size_t kHostPiece = size_t(1) << 16;  // pairs per piece of bn_pairing_many's host pipeline
+// pairs per piece of bn_pairing_many's host pipeline: 2^17 once a call has two
+// such pieces, else 2^16 (the pipeline starts above one 2^16 piece).  Piece-size
+// A/B on host buffers (profiles/r2av_host_piece_ab.jsonl): 2^17 pieces 159-162 ms
+// at 2^20 pairs and 81-83 ms at 2^19, against 168-177 / 97 ms for 2^16 pieces and
+// 163-172 / 83 ms for 2^18.
+constexpr size_t kHostPiece = size_t(1) << 17;
+constexpr size_t kHostPieceSmall = size_t(1) << 16;
 size_t round256(size_t b) { return (b + 255) & ~(size_t)255; }
 // pinned bounce buffers of bn_pairing_many (grown, never shrunk); the caller
 // has drained the copy streams, which are the buffers' only device users
@@ -531,6 +537,11 @@ int bn_ctx_create(int device, bn_ctx** out) {
     if (const char* e = getenv("BN254MI_FE_WIDE_MAX")) c->fe_wide_max = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("BN254MI_MILLER_FORM")) c->miller_form = atoi(e);
     if (const char* e = getenv("BN254MI_HOST_PIPELINE")) c->host_pipeline = atoi(e);
+    c->host_piece = kHostPiece;
+    if (const char* e = getenv("BN254MI_HOST_PIECE")) {
+        const size_t v = (size_t)strtoull(e, nullptr, 10);
+        if (v > 0 && v <= kChunk) c->host_piece = v;
+    }
     c->prepare_wide_max = kPrepareWideMaxDefault;
     if (const char* e = getenv("BN254MI_PREPARE_WIDE_MAX")) c->prepare_wide_max = (size_t)strtoull(e, nullptr, 10);
     Prog P;
@@ -710,7 +721,7 @@ int bn_get_phase_times(bn_ctx* c, float* ms, int* launches) {
     return BN_OK;
 }
 
-// bn_pairing_many on host buffers: pieces of up to kHostPiece pairs flow
+// bn_pairing_many on host buffers: pieces of 2^16 or 2^17 pairs flow
 // through two pinned bounce buffers and two device staging halves.  Piece k's
 // inputs are copied by host threads into pinned half k&1, DMA'd on the h2d
 // stream, computed on the context stream and DMA'd back on the d2h stream,
@@ -718,7 +729,7 @@ int bn_get_phase_times(bn_ctx* c, float* ms, int* launches) {
 // hipMemcpyAsync of the caller's buffers: DESIGN.md §8).  The caller's lock is
 // held throughout.
 static int pairing_many_host(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* out) {
-    const size_t piece = n < kHostPiece ? n : kHostPiece;
+    const size_t piece = n >= 2 * c->host_piece ? c->host_piece : std::min(n, kHostPieceSmall);
     const size_t o_q = round256(piece * sizeof(bn_g1));
     const size_t o_out = o_q + round256(piece * sizeof(bn_g2));
     const size_t half = o_out + round256(piece * sizeof(bn_gt));
@@ -792,7 +803,7 @@ int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* 
     // one piece has nothing to overlap, and the runtime's own pageable copies
     // measured ~6 % faster there (12.0 vs 12.6 ms at 2^16 pairs); the pipeline
     // wins from two pieces on (2^20: 171 vs 191-199 ms; profiles/r2ak_host_e2e_ab.jsonl)
-    const bool pipe = c->host_pipeline == 2 || (c->host_pipeline == 1 && n > kHostPiece);
+    const bool pipe = c->host_pipeline == 2 || (c->host_pipeline == 1 && n > kHostPieceSmall);
     const int rc = pipe ? pairing_many_host(c, p, q, n, out) : pairing_many_pageable(c, p, q, n, out);
     // an early error may leave copies queued: nothing may still touch the pinned
     // or staging buffers when the call returns

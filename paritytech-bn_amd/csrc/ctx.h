@@ -47,6 +47,7 @@ struct bn_ctx {
     // $BN254MI_HOST_PIPELINE: 1 (default) pipeline above one piece, 0 never
     // (pageable A/B form), 2 always
     int host_pipeline = 1;
+    size_t host_piece = 0;  // pairs per piece (kHostPiece; $BN254MI_HOST_PIECE, at most kChunk)
     size_t pin_bytes = 0;
     void* pin = nullptr;
     hipStream_t h2d = nullptr, d2h = nullptr;

@@ -54,18 +54,18 @@ def test_pipeline_matches_device_path_and_oracle(setup):
     assert np.array_equal(got[PIECE + 3], O.canon_to_mont_array([1] + [0] * 11))
 
 
-def _ctx_with(mode):
-    """a context created under $BN254MI_HOST_PIPELINE=mode (read at creation)"""
+def _ctx_with(mode, var="BN254MI_HOST_PIPELINE"):
+    """a context created under $var=mode (read at creation)"""
     from substrate_bn import Context
-    old = os.environ.get("BN254MI_HOST_PIPELINE")
-    os.environ["BN254MI_HOST_PIPELINE"] = mode
+    old = os.environ.get(var)
+    os.environ[var] = mode
     try:
         return Context(0)
     finally:
         if old is None:
-            del os.environ["BN254MI_HOST_PIPELINE"]
+            del os.environ[var]
         else:
-            os.environ["BN254MI_HOST_PIPELINE"] = old
+            os.environ[var] = old
 
 
 @pytest.fixture(scope="module")
@@ -87,3 +87,12 @@ def test_pageable_form_agrees(setup, n):
     _, p, q, want = setup
     ctx0 = _ctx_with("0")
     assert np.array_equal(ctx0.pairing_many(p[:n], q[:n]), want[:n])
+
+
+def test_large_piece_path(setup):
+    """the large-piece branch (pieces of host_piece once a call holds two of
+    them; 2^17 by default, 2^15 here so the fixture exercises it): seven pieces,
+    the last of 5 pairs"""
+    _, p, q, want = setup
+    ctx = _ctx_with(str(PIECE // 2), "BN254MI_HOST_PIECE")
+    assert np.array_equal(ctx.pairing_many(p, q), want)
