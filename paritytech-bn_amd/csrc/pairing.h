@@ -41,6 +41,14 @@ BN_INLINE void g2_precompute(const G2Aff<B>& q, Emit&& emit) {
     emit(k++, mixed_addition_step(r, q2));
 }
 
+#ifndef BN_LINE_ORDER
+// 1 (default): outputs last-first, each xi*f_k made just before its first use; 0:
+// first-first with the four xi*f_k up front.  Under round 1's max-ilp scheduler
+// last-first spilled less but ran 2-3 % slower (profiles/r2ai_ab_line_lazy.txt);
+// under the default scheduler it is faster: k_pairing_fused 4.31 vs 4.34 ms,
+// config 5 2.65 vs 2.70 ms (profiles/r2ax_ab_line_order.txt)
+#define BN_LINE_ORDER 1
+#endif
 #if BN_SPLIT
 // The same product f * (x0 + x4 w^3 + x2 w^4) on the two-lane layout, as six
 // column sums reduced once each.  In the w-basis (f_m = coefficient of w^m:
@@ -78,7 +86,6 @@ BN_INLINE Fq12<2> fq12_mul_by_024_lazy(const Fq12<F>& f_in, const Fq2<X>& x0_in,
     const Fq<2> f0 = widen<2>(f_in.c0.c0.c), f1 = widen<2>(f_in.c1.c0.c), f2 = widen<2>(f_in.c0.c1.c);
     const Fq<2> f3 = widen<2>(f_in.c1.c1.c), f4 = widen<2>(f_in.c0.c2.c), f5 = widen<2>(f_in.c1.c2.c);
     auto xi = [](const Fq<2>& u) { return fq2_fold(fq2_mul_xi(Fq2<2>{u})).c; };
-    const Fq<2> g2 = xi(f2), g3 = xi(f3), g4 = xi(f4), g5 = xi(f5);
     // value per lane <= 3 * (2p * 4p + 2p * 5p) = 54 p^2: the reduction is below 1.4 p
     auto out = [&](const Fq<2>& a, const LineOps& va, const Fq<2>& b, const LineOps& vb, const Fq<2>& c,
                    const LineOps& vc) {
@@ -88,15 +95,26 @@ BN_INLINE Fq12<2> fq12_mul_by_024_lazy(const Fq12<F>& f_in, const Fq2<X>& x0_in,
         acc_mad2(t, c, vc);
         return Fq2<2>{acc_redc<2>(t)};
     };
-    // (computing the outputs last-first with each xi*f_k made just before its first
-    // use spills less -- 352 vs 392 B per lane -- but ran 2-3 % slower:
-    // profiles/r2ai_ab_line_lazy.txt)
+#if BN_LINE_ORDER
+    const Fq2<2> o5 = out(f5, x0, f2, x4, f1, x2);
+    const Fq2<2> o4 = out(f4, x0, f1, x4, f0, x2);
+    const Fq<2> g5 = xi(f5);
+    const Fq2<2> o3 = out(f3, x0, f0, x4, g5, x2);
+    const Fq<2> g4 = xi(f4);
+    const Fq2<2> o2 = out(f2, x0, g5, x4, g4, x2);
+    const Fq<2> g3 = xi(f3);
+    const Fq2<2> o1 = out(f1, x0, g4, x4, g3, x2);
+    const Fq<2> g2 = xi(f2);
+    const Fq2<2> o0 = out(f0, x0, g3, x4, g2, x2);
+#else
+    const Fq<2> g2 = xi(f2), g3 = xi(f3), g4 = xi(f4), g5 = xi(f5);
     const Fq2<2> o0 = out(f0, x0, g3, x4, g2, x2);
     const Fq2<2> o1 = out(f1, x0, g4, x4, g3, x2);
     const Fq2<2> o2 = out(f2, x0, g5, x4, g4, x2);
     const Fq2<2> o3 = out(f3, x0, f0, x4, g5, x2);
     const Fq2<2> o4 = out(f4, x0, f1, x4, f0, x2);
     const Fq2<2> o5 = out(f5, x0, f2, x4, f1, x2);
+#endif
     return {{o0, o2, o4}, {o1, o3, o5}};
 }
 #endif
