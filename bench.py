@@ -149,6 +149,55 @@ def cpu_baseline(p_host, q_host, gpu_out, cpus, single_sample=1024):
             "parity_sample_bit_exact": bool(np.array_equal(ref, gpu_out) and np.array_equal(ref1, gpu_out[:m1]))}
 
 
+def sample_blocks(total, rows=4096, block=128):
+    """Global row ranges of a `rows`-row checker sample: `rows // block` blocks of
+    `block` consecutive rows spread evenly over [0, total), so every rank's shard
+    holds some (first and last rows included)."""
+    nb = max(1, min(rows // block, total // block))
+    block = min(block, total)
+    starts = sorted({(k * (total - block)) // max(nb - 1, 1) for k in range(nb)})
+    return [(a, min(a + block, total)) for a in starts]
+
+
+def gathered_sample_check(eng, rows_all, total, cpus, single=256):
+    """Rank 0's checker leg for config 4: rebuild the inputs of ~4096 rows spread
+    over every rank's shard, recompute them on the CPU (the oracle) and compare
+    with the rows this rank holds after the all-gather; the same oracle run,
+    timed, is the cpu_baseline (all usable cores, plus one core on `single` rows)."""
+    blocks = sample_blocks(total)
+    ps, qs, got = [], [], []
+    for a, b in blocks:
+        P, Q = eng.points(a, b - a)
+        ps.append(eng.host(P))
+        qs.append(eng.host(Q))
+        got.append(eng.host(rows_all[a:b]))
+    p_h, q_h, g_h = np.concatenate(ps), np.concatenate(qs), np.concatenate(got)
+    threads = cpus["usable"]
+    eng.reference(p_h[:16], q_h[:16], threads)  # warm
+    t0 = time.perf_counter()
+    ref = eng.reference(p_h, q_h, threads)
+    dt = time.perf_counter() - t0
+    m1 = min(single, p_h.shape[0])
+    t0 = time.perf_counter()
+    ref1 = eng.reference(p_h[:m1], q_h[:m1], 1)
+    dt1 = time.perf_counter() - t0
+    mism = int((ref != g_h).any(axis=1).sum())
+    check = {"rows": int(p_h.shape[0]), "blocks": len(blocks), "block_rows": blocks[0][1] - blocks[0][0],
+             "first_row": blocks[0][0], "last_row": blocks[-1][1] - 1, "mismatches": mism,
+             "parity_sample_bit_exact": bool(mism == 0 and np.array_equal(ref1, g_h[:m1])),
+             "what": "rank 0 rebuilds the inputs of the sampled global rows, recomputes them with the CPU oracle and "
+                     "compares with the Gt rows it holds after the all-gather (every rank's shard is sampled)"}
+    base = {"value": p_h.shape[0] / dt, "unit": "pairings/s", "cores": threads,
+            "kind": "dry-run stub" if eng.dry else "port",
+            "single_core": {"value": m1 / dt1, "unit": "pairings/s", "sample": "%d pairings, 1 thread" % m1},
+            "cpu_model": cpus["model"], "cpus_visible": cpus["visible"], "cpus_usable": threads,
+            "sample": "the %d-row checker sample of the gathered output, %s, %d threads (one pairing per thread), "
+                      "%.2f s wall" % (p_h.shape[0], "the dry run's stub row mix on the host" if eng.dry else
+                                       "oracle/bn_oracle.c (C restatement of substrate-bn 0.6.0)", threads, dt),
+            "parity_sample_bit_exact": check["parity_sample_bit_exact"]}
+    return check, base
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -235,6 +284,19 @@ def other_workload(args, local_rank):
                                "parity_bit_exact": bool(np.array_equal(ref, gout.cpu().numpy().view(np.uint64))
                                                         and int(gst.item()) == 0)}
     elif args.workload == "g1mul":
+        # ~3,800 Fq-mul per random 254-bit scalar (253 doublings x 7 + ~127 additions
+        # x 16), x128 MAD32; the kernel is the only launch of the step (HIP events on its stream)
+        ms = e0.elapsed_time(e1) / args.steps
+        work = n * 3800 * MAD32_PER_FQMUL
+        res["roofline"] = {"bound": "valu", "achieved": work / (ms * 1e-3) / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
+                           "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)",
+                           "frac": work / (ms * 1e-3) / PEAK_MAD32_PER_S, "traffic": pmc_traffic("k_g1_mul"),
+                           "traffic_source": "profiles/pmc_summary.json (committed PMC run, not this run)",
+                           "kernel": "k_g1_mul", "per_launch_ms": ms,
+                           "basis": "SURVEY.md 8(d) config 3: 3,800 Fq-mul per G1*Fr, x128 MAD32",
+                           "executed": "the reference chain on every lane: each of the 256 bits runs the doubling "
+                                       "(7 Fq-mul) and, when any lane of the wave has the bit set, the masked "
+                                       "addition (16 Fq-mul) -- ~5,800 Fq-mul executed per lane for random scalars"}
         m = min(args.cpu_sample or 2048, n)
         threads = host_cpus()["usable"]
         ph, kh, oh = (t[:m].cpu().numpy().view(np.uint64) for t in (P, k2, out))
@@ -384,6 +446,12 @@ class GpuEngine:
     def host(t):
         return t.cpu().numpy().view(np.uint64)
 
+    @staticmethod
+    def reference(p, q, threads):
+        """The checker: oracle/bn_oracle.c (C restatement of the reference CPU path)."""
+        from oracle import oracle as O
+        return O.pairing_many(p, q, threads)
+
 
 class DryEngine:
     """--dry-run-cpu only: exercises bench.py's launch, sharding, all-gather,
@@ -416,6 +484,15 @@ class DryEngine:
     @staticmethod
     def host(t):
         return t.numpy().view(np.uint64)
+
+    @staticmethod
+    def reference(p, q, threads):
+        """The dry run's checker: the stub's row mix recomputed on host arrays."""
+        out = np.empty((p.shape[0], 48), np.uint64)
+        out[:, :12] = p
+        out[:, 12:36] = q
+        out[:, 36:] = p ^ q[:, :12]
+        return out
 
 
 def run_pairing(args, eng, rank, world, dist):
@@ -509,10 +586,20 @@ def run_pairing(args, eng, rank, world, dist):
         res["roofline"] = {
             "bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
             "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)", "frac": achieved / PEAK_MAD32_PER_S,
-            "traffic": pmc_traffic(dom), "kernel": dom, "pairs_per_launch": chunk, "basis": FQMUL_BASIS,
+            "traffic": pmc_traffic(dom),
+            "traffic_source": "profiles/pmc_summary.json: HBM bytes per launch from the committed rocprofv3 PMC "
+                              "passes (FETCH_SIZE x2 + WRITE_SIZE), not measured in this run",
+            "kernel": dom, "pairs_per_launch": chunk, "basis": FQMUL_BASIS,
             "per_launch_ms": {k: round(v, 4) for k, v in per_launch_ms.items()},
             "whole_pairing_frac": value / world * sum(FQMUL_PER_PAIRING.values()) * MAD32_PER_FQMUL
             / PEAK_MAD32_PER_S}
+
+    if world > 1:
+        # the world size as the communicator sees it: an all-reduce of one per rank
+        one = torch.ones(1, dtype=torch.int64, device=getattr(eng, "dev", "cpu"))
+        dist.all_reduce(one)
+        res["collective"] = {"backend": dist.get_backend(), "world_from_allreduce": int(one.item()),
+                             "what": "RCCL (torch nccl backend) on GPUs; gloo in the CPU dry run"}
 
     # cross-rank equality: rebuild a sample of the next rank's rows here and compare
     # this GPU's results with what the all-gather delivered
@@ -534,7 +621,11 @@ def run_pairing(args, eng, rank, world, dist):
                                    "what": "each rank recomputes rows of the next rank's shard on its own GPU "
                                            "and compares them with the all-gathered Gt"}
 
-    if rank == 0 and world == 1 and gpu and not args.no_cpu_baseline:
+    if rank == 0 and (world > 1 or args.config == 4) and not args.no_cpu_baseline:
+        # config 4's checker leg over the gathered rows (every shard sampled) + the CPU baseline
+        res["sample_check"], res["cpu_baseline"] = gathered_sample_check(eng, gathered if world > 1 else out,
+                                                                         total, host_cpus())
+    if rank == 0 and world == 1 and args.config == 2 and gpu and not args.no_cpu_baseline:
         m = min(args.cpu_sample or 16384, local_n)
         p_h, q_h, o_h = (eng.host(t[:m]) for t in (P, Q, out))
         res["cpu_baseline"] = cpu_baseline(p_h, q_h, o_h, host_cpus())
@@ -551,7 +642,41 @@ def run_pairing(args, eng, rank, world, dist):
         res["host_buffer_e2e"] = {"value": local_n / dt, "unit": "pairings/s", "ms_per_call": dt * 1e3,
                                   "what": "bn_pairing_many on pageable host buffers, H2D + kernels + D2H, median of 5 after a warm call (one 2^16 piece takes the runtime's pageable copies; larger calls the pinned double-buffered pipeline, tools/host_e2e.py)",
                                   "matches_hbm_path": bool(np.array_equal(o_h, eng.host(out)))}
+    if rank == 0 and world == 1 and args.config == 2 and gpu and not args.no_config4_ref:
+        res["config4_on_1_gpu"] = config4_on_one_gpu(args, eng)
     return res
+
+
+def config4_on_one_gpu(args, eng, steps=3):
+    """The N = 1 point of config 4's strong-scaling curve: the same 2^20 rows,
+    chunking and kernels as a rank of `--gpus N` (no all-gather), on this GPU.
+    Reported beside `value` (which stays config 2, BASELINE's N = 1 metric)."""
+    total = args.total
+    chunk = min(total, args.chunk)
+    P, Q = eng.points(0, total)
+    out = eng.empty_gt(total)
+    bounds = [(c0, min(c0 + chunk, total)) for c0 in range(0, total, chunk)]
+
+    def step():
+        for c0, c1 in bounds:
+            eng.pairing(P[c0:c1], Q[c0:c1], out[c0:c1])
+
+    step()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.sync()
+    el = time.perf_counter() - t0
+    r = {"value": total * steps / el, "unit": "pairings/s", "total_pairs": total, "chunk": chunk, "steps": steps,
+         "ms_per_step": el / steps * 1e3,
+         "what": "BASELINE config 4's workload (%d pairs in %d-pair launches) on one GPU, no exchange: the "
+                 "same-workload N = 1 reference for the --gpus N lines" % (total, chunk)}
+    if not args.no_cpu_baseline:
+        check, _ = gathered_sample_check(eng, out, total, host_cpus())
+        r["sample_check"] = {k: check[k] for k in ("rows", "mismatches", "parity_sample_bit_exact")}
+    del P, Q, out
+    return r
 
 
 def spawn_ranks(args):
@@ -583,6 +708,8 @@ def main():
                     help="oracle sample size (default: 16384 pairings, 2048 for the 8(f) workloads; ~10-30 s of CPU-thread work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) figure")
+    ap.add_argument("--no-config4-ref", action="store_true",
+                    help="skip config 4's workload on one GPU (the same-workload N = 1 point) in the N = 1 line")
     ap.add_argument("--dry-run-cpu", action="store_true",
                     help="control-flow check on CPU: gloo + a stub engine (no pairing is computed)")
     ap.add_argument("--workload", default="pairing",

@@ -349,7 +349,7 @@ int run_fe(bn_ctx* c, const uint32_t* f, size_t n, const uint8_t* flags, bn_gt* 
         return BN_OK;
     }
     if (f != c->slots) return fail(c, BN_ERR_INVALID_ARGUMENT, "internal: step-machine FE input must be slot 0");
-    k_fq12_vm<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, n);
+    k_fq12_vm<<<grid_pair(kPathLanes * n), kPairBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, n);
     HIPCHK(c, hipGetLastError());
     k_fe_out<<<grid_for(kPathLanes * n), kBlock, 0, s>>>(c->slots, n, c->fe_out, flags, out, ok, c->d_err);
     HIPCHK(c, hipGetLastError());
@@ -523,6 +523,8 @@ static int staged(bn_ctx* c, size_t n, std::initializer_list<HostIn> ins, std::i
 }
 #define KL(kernel, ...) kernel<<<grid_for(m), kBlock, 0, s>>>(__VA_ARGS__)
 
+static void ctx_teardown(bn_ctx* c);
+
 extern "C" {
 
 int bn_ctx_create(int device, bn_ctx** out) {
@@ -549,7 +551,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
     P.finalize({(uint32_t)c->fe_out});
     c->fe_steps = P.steps();
     if (P.next > (uint32_t)kFeSlots) {
-        delete c;
+        delete c;  // nothing created yet
         return BN_ERR_INVALID_ARGUMENT;
     }
     bool events_ok = true;
@@ -564,7 +566,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
         hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess ||
         hipMalloc(&c->d_prog, P.s.size() * 4) != hipSuccess ||
         hipMemcpy(c->d_prog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
-        delete c;
+        ctx_teardown(c);  // releases whatever was created (null handles are skipped)
         return BN_ERR_HIP;
     }
     *out = c;
@@ -574,9 +576,18 @@ int bn_ctx_create(int device, bn_ctx** out) {
 int bn_ctx_destroy(bn_ctx* c) {
     if (!c) return BN_ERR_INVALID_ARGUMENT;
     if (!c->subs.empty()) return bn_multi_destroy(c);
+    ctx_teardown(c);
+    return BN_OK;
+}
+
+}  // extern "C"
+
+// releases every resource of a single-device context (also a partially created
+// one: null handles are skipped) and deletes it
+static void ctx_teardown(bn_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->ws_pending) (void)hipEventSynchronize(c->ws_event);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (hipStream_t s : {c->h2d, c->d2h})
         if (s) (void)hipStreamSynchronize(s);
     if (c->ws_event) (void)hipEventDestroy(c->ws_event);
@@ -592,10 +603,11 @@ int bn_ctx_destroy(bn_ctx* c) {
         for (auto e : ev) c->ev_pool.push_back(e);
     for (auto e : c->ev_pool)
         if (e) (void)hipEventDestroy(e);
-    (void)hipStreamDestroy(c->stream);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
-    return BN_OK;
 }
+
+extern "C" {
 
 const char* bn_last_error(const bn_ctx* c) { return c ? c->err.c_str() : "null context"; }
 void* bn_ctx_stream(bn_ctx* c) { return c ? (void*)c->stream : nullptr; }
@@ -656,7 +668,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             continue;
         }
         if (c->miller_form == 1) {
-            k_pairing_fused<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->flags, c->d_err, 0,
+            k_pairing_fused<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(d_p + off, d_q + off, m, c->flags, c->d_err, 0,
                                                                         c->slots);
             mark(1);
         } else {
@@ -672,15 +684,11 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             }
         }
         mark(2);
-        if (m <= c->fe_wide_max) {  // latency: 16 lanes per element (kernels_wide.hip)
-            k_fe_wide<<<grid_for(16 * m), kBlock, 0, s>>>(c->slots, m, m, d_out + off, nullptr, c->d_err);
-            mark(3);
-        } else {
-            k_fq12_vm<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, m);
-            mark(3);
-            k_fe_out<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->slots, m, c->fe_out, c->flags, d_out + off, nullptr,
-                                                                 c->d_err);
-        }
+        // (m > fe_wide_max here: smaller chunks took the latency path above)
+        k_fq12_vm<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(c->d_prog, c->fe_steps, c->slots, m);
+        mark(3);
+        k_fe_out<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->slots, m, c->fe_out, c->flags, d_out + off, nullptr,
+                                                             c->d_err);
         mark(4);
         HIPCHK(c, hipGetLastError());
         if (c->timing) c->ev_marks.push_back(ev);
@@ -916,9 +924,10 @@ static int batch_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn
     WsUse use{c, s};
     HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int), s));
     if (n == 0) {  // pairing_batch: mod.rs:922-924; the shared loop starts from one (mod.rs:610)
-        static bn_gt one;
-        bn_internal_gt_one(&one);
-        HIPCHK(c, hipMemcpyAsync(d_out, &one, sizeof(bn_gt), hipMemcpyHostToDevice, s));
+        // a constant-initialized, read-only image: no thread ever writes it
+        static const bn_gt kGtOne = {{{{0xd35d438dc58f0d9dull, 0x0a78eb28f5c70b3dull, 0x666ea36f7879462cull,
+                                        0x0e0a77c19a07df2full}}}};
+        HIPCHK(c, hipMemcpyAsync(d_out, &kGtOne, sizeof(bn_gt), hipMemcpyHostToDevice, s));
     } else {
         RET_IF(miller_product_dev(c, d_p, d_q, n, mode, d_out, s));
     }
@@ -1073,7 +1082,7 @@ int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n,
         }
         P.finalize({res});
         HIPCHK(c, hipMemcpyAsync(dprog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice, c->stream));
-        k_fq12_vm<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(dprog, P.steps(), c->slots, m);
+        k_fq12_vm<<<grid_pair(kPathLanes * m), kPairBlock, 0, c->stream>>>(dprog, P.steps(), c->slots, m);
         k_gt_store<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(c->slots + (size_t)res * kSlotWords * m, m, m, dout);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(out + off, dout, m * sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));

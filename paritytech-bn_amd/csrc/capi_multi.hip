@@ -28,9 +28,22 @@
 namespace {
 
 int mfail(bn_ctx* c, int code, const std::string& msg) {
-    if (c) c->err = msg;
+    if (c) {
+        std::lock_guard<std::mutex> g(c->err_mu);
+        c->err = msg;
+    }
     return code;
 }
+// restores the calling thread's current device on scope exit
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
 
 // contiguous shard k of n over d parts (the same split as substrate_bn/parallel.py)
 void shard(size_t n, size_t d, size_t k, size_t* lo, size_t* hi) {
@@ -165,6 +178,7 @@ int bn_pairing_many_allgather_dev(bn_ctx* c, const bn_g1* const* d_p, const bn_g
     const size_t d = subs.size();
     if (n_per_dev == 0) return BN_OK;
     std::lock_guard<std::mutex> lock(c->mu);  // the multi context's own lock: one collective at a time
+    DeviceGuard keep_device;                  // the sub-context calls and the gather switch devices
     std::vector<hipStream_t> st(d);
     for (size_t k = 0; k < d; ++k) {
         st[k] = streams && streams[k] ? (hipStream_t)streams[k] : (hipStream_t)bn_ctx_stream(subs[k]);
@@ -176,12 +190,15 @@ int bn_pairing_many_allgather_dev(bn_ctx* c, const bn_g1* const* d_p, const bn_g
     if (int rc = comms_get(c, &cm)) return rc;
     cm->r.group_start();
     int e = 0;
-    for (size_t k = 0; k < d && !e; ++k) {
-        if (hipSetDevice(c->devices[k]) != hipSuccess) return mfail(c, BN_ERR_HIP, "hipSetDevice");
-        e = cm->r.all_gather(d_out[k] + k * n_per_dev, d_out[k], n_per_dev * sizeof(bn_gt), kNcclUint8, cm->comm[k],
-                             st[k]);
+    bool dev_ok = true;
+    for (size_t k = 0; k < d && !e && dev_ok; ++k) {
+        dev_ok = hipSetDevice(c->devices[k]) == hipSuccess;
+        if (dev_ok)
+            e = cm->r.all_gather(d_out[k] + k * n_per_dev, d_out[k], n_per_dev * sizeof(bn_gt), kNcclUint8,
+                                 cm->comm[k], st[k]);
     }
-    const int e2 = cm->r.group_end();
+    const int e2 = cm->r.group_end();  // always closes the group, also after an error above
+    if (!dev_ok) return mfail(c, BN_ERR_HIP, "hipSetDevice");
     if (e || e2) return mfail(c, BN_ERR_HIP, std::string("ncclAllGather: ") + cm->r.error_string(e ? e : e2));
     return BN_OK;
 }

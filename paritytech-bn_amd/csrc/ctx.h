@@ -12,6 +12,10 @@ struct bn_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
+    // last error message; a multi-device context's host-buffer calls write it
+    // without holding `mu` (their sub-contexts do the locking), so writes there
+    // take err_mu
+    std::mutex err_mu;
     std::string err;
     // workspace (device)
     size_t cap = 0;  // pairings

@@ -123,11 +123,11 @@ BN_INLINE Jac<F> jac_double(const Jac<F>& s) {
     return {narrow<kPt>(x3), narrow<kPt>(F_sub(F_mul(e, F_sub(F_fold(d), x3)), eight_c)), narrow<kPt>(F_add(y1z1, y1z1))};
 }
 
-// mod.rs:294-334, including both zero short-cuts and the doubling branch
+// mod.rs:294-334, including both zero short-cuts and the doubling branch;
+// o_zero = jac_is_zero(o), computed once by a caller that adds the same o often
 template <template <int> class F>
-BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o) {
+BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o, bool o_zero) {
     const bool s_zero = jac_is_zero(s);
-    const bool o_zero = jac_is_zero(o);
     auto z1_squared = F_sqr(s.z);
     auto z2_squared = F_sqr(o.z);
     auto u1 = F_mul(s.x, z2_squared);
@@ -159,6 +159,11 @@ BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o) {
     return out;
 }
 
+template <template <int> class F>
+BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o) {
+    return jac_add(s, o, jac_is_zero(o));
+}
+
 // mod.rs:336-350
 template <template <int> class F>
 BN_INLINE Jac<F> jac_neg(const Jac<F>& a) {
@@ -174,6 +179,7 @@ template <template <int> class F>
 BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8]) {
     Jac<F> res = jac_zero<F>();
     bool found_one = false;
+    const bool p_zero = jac_is_zero(p);
     uint32_t w[8];  // scalar, shifted left one bit per step (no indexed private arrays)
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = k[i];
@@ -188,7 +194,7 @@ BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8]) {
             res = {F_select(found_one, d.x, res.x), F_select(found_one, d.y, res.y), F_select(found_one, d.z, res.z)};
         }
         if (BN_ANY(b)) {
-            Jac<F> a = jac_add(res, p);
+            Jac<F> a = jac_add(res, p, p_zero);
             res = {F_select(b, a.x, res.x), F_select(b, a.y, res.y), F_select(b, a.z, res.z)};
             found_one = found_one || b;
         }

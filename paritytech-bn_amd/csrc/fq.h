@@ -557,21 +557,25 @@ template <int B>
 BN_INLINE Fq<1> fq_canonical(const Fq<B>& a) {
     return fq_cond_sub_p(widen<2>(fq_reduce(a)));
 }
+// a == 0 (mod p) without a product: the fold leaves a normalized value
+// x <= 2p with the same residue, and x == 0 (mod p) iff x is 0, p or 2p (three
+// digit-wise compares; about half the instructions of fq_canonical's REDC)
 template <int B>
 BN_INLINE bool fq_is_zero(const Fq<B>& a) {
-    Fq<1> c = fq_canonical(a);
-    uint32_t o = 0;
+    const Fq<2> x = fq_fold(a);
+    constexpr Limbs9 P1 = kp_plain(1), P2 = kp_plain(2);
+    uint32_t o0 = 0, o1 = 0, o2 = 0;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) o |= c.v[i];
-    return o == 0;
+    for (int i = 0; i < 9; ++i) {
+        o0 |= x.v[i];
+        o1 |= x.v[i] ^ P1.v[i];
+        o2 |= x.v[i] ^ P2.v[i];
+    }
+    return (o0 == 0) | (o1 == 0) | (o2 == 0);
 }
 template <int A, int B>
 BN_INLINE bool fq_eq(const Fq<A>& a, const Fq<B>& b) {
-    Fq<1> x = fq_canonical(a), y = fq_canonical(b);
-    uint32_t o = 0;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) o |= x.v[i] ^ y.v[i];
-    return o == 0;
+    return fq_is_zero(fq_sub(a, b));
 }
 
 // ---------------------------------------------------------------- boundary

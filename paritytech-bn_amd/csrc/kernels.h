@@ -384,6 +384,64 @@ __device__ __forceinline__ void fr_to_canonical(const bn_fr& k, uint32_t out[8])
 
 __device__ __forceinline__ size_t lane_id() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
+// ---------------------------------------------------------------- two-wave issue balance
+// The throughput kernels (k_pairing_fused, k_fq12_vm) run exactly two waves per
+// SIMD, both issue-bound on VALU.  The SIMD arbitrates VALU issue between them by
+// priority, then age (MI355X_MICROARCH.md, "Two waves per SIMD"), so at equal
+// priority the older wave runs ahead and the younger one finishes its second half
+// ALONE, at the lone-wave issue rate: the measured average wave lifetime was
+// ~0.77 of the kernel (profiles/pmc_summary.json).
+// Balance: these kernels launch kPairBlock = 512 threads, i.e. one workgroup of
+// eight waves per CU holding both waves of each SIMD.  Each wave publishes its
+// program position in LDS at every step of its main loop and raises its priority
+// (s_setprio 1) while it is not ahead of the other wave on its SIMD (found from
+// HW_ID's SIMD field at start), else drops to 0 -- so the two waves alternate the
+// lead and finish together.  Scheduling only: no value depends on it.
+// BN_BALANCE=0 builds the plain form (A/B).
+#ifndef BN_BALANCE
+#define BN_BALANCE 1
+#endif
+#ifndef BN_PAIR_BLOCK
+#define BN_PAIR_BLOCK 512
+#endif
+constexpr int kPairBlock = BN_PAIR_BLOCK;
+struct Balance {
+    uint32_t w = 0, partner = 0;
+};
+#if BN_BALANCE && defined(__HIP_DEVICE_COMPILE__)
+__shared__ uint32_t g_bal_prog[kPairBlock / 64];
+__shared__ uint32_t g_bal_simd[kPairBlock / 64];
+// every thread of the block calls this (it has a barrier), before any early return
+__device__ __forceinline__ Balance balance_init() {
+    Balance b;
+    b.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // HW_ID (hwreg 4): bits 5:4 = the SIMD this wave runs on
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    g_bal_simd[b.w] = (hw >> 4) & 3u;
+    g_bal_prog[b.w] = 0;
+    __syncthreads();
+    const uint32_t nw = blockDim.x >> 6;
+    b.partner = b.w;
+    for (uint32_t j = 0; j < nw; ++j)
+        if (j != b.w && g_bal_simd[j] == g_bal_simd[b.w]) b.partner = j;
+    b.partner = __builtin_amdgcn_readfirstlane(b.partner);
+    return b;
+}
+// `pos`: this wave's position in the (shared) program, non-decreasing
+__device__ __forceinline__ void balance_step(const Balance& b, uint32_t pos) {
+    volatile uint32_t* pr = g_bal_prog;
+    pr[b.w] = pos;
+    const uint32_t other = __builtin_amdgcn_readfirstlane(pr[b.partner]);
+    if (pos > other)
+        __builtin_amdgcn_s_setprio(0);
+    else
+        __builtin_amdgcn_s_setprio(1);
+}
+#else
+__device__ __forceinline__ Balance balance_init() { return Balance{}; }
+__device__ __forceinline__ void balance_step(const Balance&, uint32_t) {}
+#endif
+
 
 // BN_DEVICE_CHECKS builds: export this translation unit's fold-bound
 // violation counter (fq.h) as bn_dbg_fold_bad_<tu>().
@@ -400,6 +458,7 @@ __device__ __forceinline__ size_t lane_id() { return (size_t)blockIdx.x * blockD
 #endif
 
 inline unsigned grid_for(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+inline unsigned grid_pair(size_t n) { return (unsigned)((n + kPairBlock - 1) / kPairBlock); }
 
 // ---------------------------------------------------------------- Fq12 step machine
 // The final exponentiation is ~300 Fq12 operations; compiled inline it is one
@@ -455,12 +514,12 @@ __global__ void __launch_bounds__(kBlock) k_prepare_wide(const bn_g1* __restrict
                                                          int* __restrict__ err, int mode);
 __global__ void __launch_bounds__(kBlock) k_coeffs_store(const uint32_t* __restrict__ coeffs, size_t n,
                                                          bn_fq2* __restrict__ out);
-__global__ void __launch_bounds__(kBlock) k_pairing_fused(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
+__global__ void __launch_bounds__(kPairBlock) k_pairing_fused(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
                                                           size_t n, uint8_t* __restrict__ flags, int* __restrict__ err,
                                                           int mode, uint32_t* __restrict__ f_out);
 __global__ void __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ coeffs, const uint32_t* __restrict__ paff,
                          const uint8_t* __restrict__ flags, size_t n, uint32_t* __restrict__ f_out);
-__global__ void __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps, uint32_t* slots, size_t n);
+__global__ void __launch_bounds__(kPairBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps, uint32_t* slots, size_t n);
 __global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot, const uint8_t* __restrict__ flags,
                          bn_gt* __restrict__ out, uint8_t* __restrict__ ok, int* __restrict__ err);
 // kernels_wide.hip (fq12_wide.h): final exponentiation and product reduction on 16-lane groups

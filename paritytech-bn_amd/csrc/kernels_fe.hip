@@ -19,9 +19,12 @@ __device__ __forceinline__ uint32_t* slot_ptr(uint32_t* slots, size_t nl, uint32
     return slots + (size_t)s * kSlotLaneWords * nl;
 }
 
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps,
-                                                                uint32_t* slots, size_t n) {
+// Launched with kPairBlock threads per block (kernels.h: two-wave issue balance;
+// the program position is step * 256 + squarings done in the step).
+__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps,
+                                                                    uint32_t* slots, size_t n) {
     fold_table_init();
+    const Balance bal = balance_init();
     const size_t i = lane_id();
     if (i >= kL * n) return;
     Fq12<kF> acc = widen<kF>(fq12_one());  // the previous step's result, kept in registers
@@ -39,6 +42,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_fq12_vm(const uint32_t*
         uint32_t* d = slot_ptr(slots, nn, (ins >> 8) & 0xff);
         const uint32_t* a = slot_ptr(slots, nn, (ins >> 16) & 0xff);
         const uint32_t* b = slot_ptr(slots, nn, ins >> 24);
+        balance_step(bal, (uint32_t)pc << 8);
         Fq12<kF> x;
         if (flags & kFlagAccA) x = acc; else x = ld_fq12_buf<kF>(a, nn, i);
         Fq12<kF> r;
@@ -46,7 +50,11 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_fq12_vm(const uint32_t*
             case OP_MOV: r = x; break;
             case OP_MUL: {
 #pragma unroll 1
-                for (uint32_t j = 0; j < k; ++j) x = cyc_sqr(x);
+                for (uint32_t j = 0; j < k; ++j) {
+                    balance_step(bal, ((uint32_t)pc << 8) | j);
+                    x = cyc_sqr(x);
+                }
+                balance_step(bal, ((uint32_t)pc << 8) | 255u);
                 Fq12<kF> y = ld_fq12_buf<kF>(b, nn, i);
                 if (flags & kFlagConjB) y = fq12_conj(y);
                 r = mul12(x, y);
@@ -56,7 +64,10 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_fq12_vm(const uint32_t*
             case OP_SQR: r = narrow12<kF>(fq12_sqr(x)); break;
             case OP_CYC: {
 #pragma unroll 1
-                for (uint32_t j = 0; j < k; ++j) x = cyc_sqr(x);
+                for (uint32_t j = 0; j < k; ++j) {
+                    balance_step(bal, ((uint32_t)pc << 8) | j);
+                    x = cyc_sqr(x);
+                }
                 r = x;
                 break;
             }

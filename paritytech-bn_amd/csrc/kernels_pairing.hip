@@ -253,16 +253,18 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_coeffs_store(const uint
 // Miller loop fused in one kernel -- each coefficient is applied as soon as it is
 // computed and never leaves registers (no 16.7 KB/pairing HBM round trip).  Same
 // operations in the same order as k_prepare + k_miller, so the same Miller value.
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_pairing_fused(const bn_g1* __restrict__ p,
-                                                                      const bn_g2* __restrict__ q, size_t n,
-                                                                      uint8_t* __restrict__ flags,
-                                                                      int* __restrict__ err, int mode,
-                                                                      uint32_t* __restrict__ f_out) {
+// Launched with kPairBlock threads per block (kernels.h: two-wave issue balance).
+__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_pairing_fused(const bn_g1* __restrict__ p,
+                                                                          const bn_g2* __restrict__ q, size_t n,
+                                                                          uint8_t* __restrict__ flags,
+                                                                          int* __restrict__ err, int mode,
+                                                                          uint32_t* __restrict__ f_out) {
     fold_table_init();
+    const Balance bal = balance_init();
     const size_t l = lane_id(), i = l / kL, nl = kL * n;
     if (i >= n) return;
     const PairAffine a = pair_to_affine(p, q, i, l, flags, err, mode);
-    Fq12<kF> f = miller_fused(a.qa, a.px, a.py);
+    Fq12<kF> f = miller_fused(a.qa, a.px, a.py, [&](int d) { balance_step(bal, (uint32_t)d); });
     if (flags[l]) f = widen<kF>(fq12_one());
     st_fq12(f_out, nl, l, f);
 }

@@ -63,18 +63,26 @@ def pairing_many_distributed_dev(P, Q, compute=None, stream=None):
     n = P.shape[0]
     lo, hi = shard_bounds(n, rank, world)
     max_rows = max(shard_bounds(n, r, world)[1] - shard_bounds(n, r, world)[0] for r in range(world))
+    # every buffer the engine reads or writes is made on torch's current stream
+    # first (the contiguous copies of a non-contiguous P or Q included), and only
+    # then does the engine stream wait for that stream
     buf = torch.zeros((max_rows, 48), dtype=torch.int64, device=P.device)
+    ps = P[lo:hi].contiguous() if hi > lo else None
+    qs = Q[lo:hi].contiguous() if hi > lo else None
     engine_stream = None
     if compute is None:
         from . import context
         ctx = context()
         engine_stream = stream if stream is not None else torch.cuda.ExternalStream(ctx.stream, device=P.device)
         engine_stream.wait_stream(torch.cuda.current_stream(P.device))  # inputs and buf are ready
+        for t in (buf, ps, qs):  # the caching allocator must not reuse them before the engine is done
+            if t is not None:
+                t.record_stream(engine_stream)
 
         def compute(a, b, out):
             ctx.pairing_many_dev(a.data_ptr(), b.data_ptr(), a.shape[0], out.data_ptr(), engine_stream.cuda_stream)
     if hi > lo:
-        compute(P[lo:hi].contiguous(), Q[lo:hi].contiguous(), buf[:hi - lo])
+        compute(ps, qs, buf[:hi - lo])
     if engine_stream is not None:
         torch.cuda.current_stream(P.device).wait_stream(engine_stream)
     gathered = torch.empty((world * max_rows, 48), dtype=torch.int64, device=P.device)

@@ -37,6 +37,27 @@ void he_fq_fold(const uint32_t* a, uint32_t* o) {
     auto big = fq_add(fq_mul_small<8>(fq_mul_small<8>(x)), fq_sub(x, widen<20>(x)));
     st(fq_fold(big), o);
 }
+// fq_is_zero / fq_eq on multiples of p with lazy digits and on plain values:
+// bit k of o[0] = test k (see tests/test_host_emul.py::test_fq_is_zero)
+void he_fq_zero_checks(const uint32_t* a, const uint32_t* b, uint32_t* o) {
+    auto x = ld(a), y = ld(b);
+    auto z1 = fq_sub(x, x);               // (B+1) p with raised digits
+    auto z2 = fq_add(z1, fq_sub(y, y));   // a larger multiple of p
+    auto z3 = fq_mul_small<4>(z1);        // 4 (B+1) p, lazy digits
+    auto z4 = fq_neg(x);                  // B p - x
+    uint32_t r = 0;
+    r |= (uint32_t)fq_is_zero(z1) << 0;
+    r |= (uint32_t)fq_is_zero(z2) << 1;
+    r |= (uint32_t)fq_is_zero(z3) << 2;
+    r |= (uint32_t)fq_is_zero(x) << 3;
+    r |= (uint32_t)fq_is_zero(fq_sub(x, y)) << 4;
+    r |= (uint32_t)fq_eq(x, fq_add(x, z3)) << 5;
+    r |= (uint32_t)fq_is_zero(fq_add(x, z4)) << 6;
+    r |= (uint32_t)fq_eq(x, y) << 7;
+    r |= (uint32_t)fq_is_zero(fq_zero()) << 8;
+    o[0] = r;
+    o[1] = 0;
+}
 void he_fq2_mul(const uint32_t* a, const uint32_t* b, uint32_t* o) { st2(fq2_mul(ld2(a), ld2(b)), o); }
 void he_fq2_sqr(const uint32_t* a, uint32_t* o) { st2(fq2_sqr(ld2(a)), o); }
 void he_fq2_inv(const uint32_t* a, uint32_t* o) { st2(fq2_inv(ld2(a)), o); }

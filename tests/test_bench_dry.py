@@ -32,6 +32,26 @@ def test_bench_spawns_ranks_config4(world):
     assert line["config"]["total_pairs"] == 16384 and line["config"]["pairs_per_gpu"] == 16384 // world
     assert line["scaling"] == "strong" and line["config"]["allgather_in_step"]
     assert line["cross_rank_check"]["mismatches"] == 0 and line["cross_rank_check"]["ranks_ok"] == world
+    # rank 0's checker leg over the gathered rows: 4096 rows spread over every shard
+    sc = line["sample_check"]
+    assert sc["rows"] == 4096 and sc["mismatches"] == 0 and sc["parity_sample_bit_exact"] is True
+    assert sc["first_row"] == 0 and sc["last_row"] == 16383
+    cb = line["cpu_baseline"]
+    assert cb["parity_sample_bit_exact"] is True and cb["value"] > 0 and cb["kind"] == "dry-run stub"
+    assert {"cores", "single_core", "cpu_model", "sample", "unit"} <= set(cb)
+    assert line["collective"]["world_from_allreduce"] == world
+
+
+def test_sample_blocks_cover_every_shard():
+    sys.path.insert(0, ROOT)
+    import bench
+    total = 1 << 20
+    blocks = bench.sample_blocks(total)
+    assert sum(b - a for a, b in blocks) == 4096 and blocks[0][0] == 0 and blocks[-1][1] == total
+    for world in (2, 4, 8):
+        per = total // world
+        assert {a // per for a, _ in blocks} == set(range(world))
+    assert bench.sample_blocks(100) == [(0, 100)]
 
 
 def test_bench_world_size_must_match_gpus():

@@ -90,6 +90,15 @@ def test_torch_distributed_forms_world_of_one(data):
         got2 = parallel.pairing_many_distributed_dev(P, Q, stream=st)
         torch.cuda.synchronize(dev)
         assert np.array_equal(got2.cpu().numpy().view(np.uint64), data["gt"])
+        # non-contiguous inputs (column views of wider tensors): the shard copies
+        # are made on torch's stream before the engine stream waits for it
+        wideP = torch.zeros((101, 20), dtype=torch.int64, device=dev)
+        wideP[:, 3:15] = P
+        wideQ = torch.zeros((101, 30), dtype=torch.int64, device=dev)
+        wideQ[:, 5:29] = Q
+        got3 = parallel.pairing_many_distributed_dev(wideP[:, 3:15], wideQ[:, 5:29], stream=st)
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(got3.cpu().numpy().view(np.uint64), data["gt"])
         assert np.array_equal(parallel.pairing_batch_distributed(data["pz"], data["q"]), data["prod"])
         assert np.array_equal(parallel.pairing_many_distributed(data["pz"], data["q"]), data["gt"])
     finally:

@@ -55,6 +55,17 @@ def test_fq_fold_value(rnd):
         assert got == [(64 * v + v - v) % O.P]
 
 
+def test_fq_is_zero(rnd):
+    """fq_is_zero / fq_eq (fold, then compare with 0, p, 2p) on multiples of p with
+    lazy digits and on plain values, including 0 and p - 1."""
+    vals = rnd(20) + [0, 1, O.P - 1]
+    for k, v in enumerate(vals):
+        w = vals[(k + 1) % len(vals)] if k % 3 else v
+        bits = int(H.call("he_fq_zero_checks", fe([v]), fe([w]), out_words=2)[0])
+        want = 0b1 | 0b10 | 0b100 | ((v == 0) << 3) | ((v == w) << 4) | (1 << 5) | (1 << 6) | ((v == w) << 7) | (1 << 8)
+        assert bits == want, (v, w, bin(bits), bin(want))
+
+
 def test_tower_vs_oracle(rnd):
     for _ in range(6):
         a = fe(rnd(12))

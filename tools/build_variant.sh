@@ -1,0 +1,17 @@
+#!/bin/bash
+# Build an A/B variant of libbn254mi.so with extra compile flags into
+# exp/lib_NAME.so (bench.py / tests load it with BN254MI_LIB=exp/lib_NAME.so).
+# Usage: tools/build_variant.sh NAME "-DFLAG=1 ..."
+set -e
+NAME=$1; FLAGS=$2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+B=$ROOT/exp/build_$NAME
+mkdir -p $B
+SRCS="kernels_pairing kernels_fe kernels_group kernels_util kernels_codec kernels_gtpow kernels_wide capi capi_multi"
+for s in $SRCS; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $FLAGS \
+    -c -o $B/$s.o $ROOT/paritytech-bn_amd/csrc/$s.hip &
+done
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $ROOT/exp/lib_$NAME.so $(for s in $SRCS; do echo $B/$s.o; done) -ldl
+echo "built exp/lib_$NAME.so"
