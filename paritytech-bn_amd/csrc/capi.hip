@@ -287,10 +287,11 @@ void par_copy(void* dst, const void* src, size_t bytes) {
 // the batch leaves the GPU underfilled, two lanes per pair (k_prepare) otherwise
 static int prepare(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int mode, hipStream_t s) {
     if (m <= c->prepare_wide_max)
-        k_prepare_wide<<<grid_for(kPrepareWideLanes * m), kBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags,
-                                                                          c->d_err, mode);
+        k_prepare_wide<<<grid_pair(kPrepareWideLanes * m), kPairBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff,
+                                                                              c->flags, c->d_err, mode);
     else
-        k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags, c->d_err, mode);
+        k_prepare<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags, c->d_err,
+                                                                   mode);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
@@ -359,20 +360,15 @@ int run_fe(bn_ctx* c, const uint32_t* f, size_t n, const uint8_t* flags, bn_gt* 
 // ---- pairing_batch / miller_loop_batch: segmented Miller loop + device reduction
 constexpr int kRegionSeg = 8;  // k_miller_seg output: S * n elements from region kRegionSeg on
 
-// S segments of the 64 NAF digits (S doubles until S * n pairs fill about
-// 2^16 lane pairs, i.e. two waves per SIMD), cut so each carries about the same
-// work: a digit costs a squaring (36 Fq-mul) and a line (39), a nonzero digit
-// one more line, the last segment the two closing lines.
-SegPlan seg_plan(size_t n) {
+// cut the 64 digits into S segments of about equal work for K pairs per lane
+// pair (a digit: one squaring, 36 Fq-mul, and K lines of 39; a nonzero digit K
+// more lines; the last segment the 2 K closing lines)
+static SegPlan cut_plan(int S, int K) {
     SegPlan p{};
-    int S = 1;
-    // S doubles while S*n lane pairs leave the GPU underfilled; 16 segments only
-    // for the smallest batches (profiles/r2ac_latency_seg16.txt: 16 helps up to
-    // ~1024 pairs, costs at 4096 through the longer Horner recombination)
-    while (S < kMaxSeg && (size_t)S * n < ((size_t)1 << 16) && !(S >= 8 && (size_t)S * n >= ((size_t)1 << 14))) S *= 2;
     p.S = S;
-    auto cost = [](int d) { return 36 + 39 + (((kNafNonzero >> d) & 1u) ? 39 : 0); };
-    int total = 2 * 39;
+    p.K = K;
+    auto cost = [K](int d) { return 36 + 39 * K + (((kNafNonzero >> d) & 1u) ? 39 * K : 0); };
+    int total = 2 * 39 * K;
     for (int d = 0; d < BN_NAF_DIGITS; ++d) total += cost(d);
     int g = 0, acc = 0;
     p.lo[0] = 0;
@@ -389,6 +385,30 @@ SegPlan seg_plan(size_t n) {
         p.idx[k] = p.lo[k] + __builtin_popcountll(kNafNonzero & ((p.lo[k] ? (1ull << p.lo[k]) : 1ull) - 1ull));
     return p;
 }
+// pairing_many's latency path: one pair per lane pair (K = 1); S doubles while
+// S*n lane pairs leave the GPU underfilled; 16 segments only for the smallest
+// batches (profiles/r2ac_latency_seg16.txt: 16 helps up to ~1024 pairs, costs
+// at 4096 through the longer Horner recombination of every pair)
+SegPlan seg_plan(size_t n) {
+    int S = 1;
+    while (S < kMaxSeg && (size_t)S * n < ((size_t)1 << 16) && !(S >= 8 && (size_t)S * n >= ((size_t)1 << 14))) S *= 2;
+    return cut_plan(S, 1);
+}
+// pairing_batch / miller_loop_batch (one Horner recombination for the whole
+// product): 16 segments, and K pairs per lane pair sharing one squaring per
+// digit (mod.rs:609-640) -- the largest K <= 16 that still leaves 16 * ceil(n/K)
+// >= 2^16 lane pairs (two waves per SIMD).  At 2^14 terms: K = 4, a lane pair
+// runs 4 digits with one squaring and ~5.3 lines each instead of 16 digits
+// with one squaring and ~1.3 lines each (S = 4, K = 1 before).
+SegPlan batch_plan(size_t n) {
+    int K = 1;
+    while (K < 16 && (size_t)kMaxSeg * ((n + 2 * K - 1) / (2 * K)) >= ((size_t)1 << 16)) K *= 2;
+    if (const char* e = getenv("BN254MI_BATCH_K")) {  // A/B: pairs per lane pair (1, 2, 4, 8, 16)
+        const int v = atoi(e);
+        if (v >= 1 && v <= 16) K = v;
+    }
+    return cut_plan(kMaxSeg, K);
+}
 
 // Segment values of m <= kChunk device pairs (mode 0: a pair with a zero point
 // counts as one; mode 1: a zero point sets the BN_ERR_TO_AFFINE bit), each
@@ -397,10 +417,11 @@ SegPlan seg_plan(size_t n) {
 int chunk_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int mode, const SegPlan& plan,
                   uint32_t* parts, size_t nchunks, size_t k, hipStream_t s) {
     RET_IF(prepare(c, d_p, d_q, m, mode, s));
-    k_miller_seg<<<grid_for(kPathLanes * plan.S * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
+    const size_t G = (m + plan.K - 1) / plan.K;  // lane-pair groups per segment
+    k_miller_seg<<<grid_pair(kPathLanes * plan.S * G), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
                                                                        slot_region(c, kRegionSeg));
     HIPCHK(c, hipGetLastError());
-    return product_wide(c, slot_region(c, kRegionSeg), plan.S * m, m, m, plan.S, parts, plan.S * nchunks, k, nchunks,
+    return product_wide(c, slot_region(c, kRegionSeg), plan.S * G, G, G, plan.S, parts, plan.S * nchunks, k, nchunks,
                         s);
 }
 // where chunk partials go: straight into the result region (element g, stride S)
@@ -423,7 +444,7 @@ int miller_product_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, 
                        hipStream_t s) {
     const size_t nchunks = (n + kChunk - 1) / kChunk;
     const size_t m0 = n < kChunk ? n : kChunk;
-    const SegPlan plan = seg_plan(m0);
+    const SegPlan plan = batch_plan(m0);
     RET_IF(reserve(c, m0));
     if (nchunks * plan.S > c->cap) return fail(c, BN_ERR_INVALID_ARGUMENT, "too many chunks");
     uint32_t* parts = parts_region(c, nchunks);
@@ -462,8 +483,21 @@ int clear_err(bn_ctx* c, hipStream_t s) {
     RET_IF(ws_acquire((ctx), (ctx)->stream)); \
     WsUse ws_use_{(ctx), (ctx)->stream}
 
+// k_g1_mul: kPairBlock-thread blocks (two waves on every SIMD, kernels.h issue
+// balance) once the batch gives every CU one such block, else kBlock
+constexpr size_t kG1MulPairBlockMin = (size_t)256 * kPairBlock;
+static void g1_mul_launch(const bn_g1* d_p, const bn_fr* d_k, size_t n, bn_g1* d_out, hipStream_t s) {
+    if (n >= kG1MulPairBlockMin)
+        k_g1_mul<<<grid_pair(n), kPairBlock, 0, s>>>(d_p, d_k, n, d_out);
+    else
+        k_g1_mul<<<grid_for(n), kBlock, 0, s>>>(d_p, d_k, n, d_out);
+}
+static void g2_mul_launch(const bn_g2* d_p, const bn_fr* d_k, size_t n, bn_g2* d_out, hipStream_t s) {
+    k_g2_mul<<<grid_for(n), kBlock, 0, s>>>(d_p, d_k, n, d_out);
+}
+
 template <typename P, typename K>
-static int host_mul(bn_ctx* c, const P* p, const bn_fr* k, size_t n, P* out, K kernel) {
+static int host_mul(bn_ctx* c, const P* p, const bn_fr* k, size_t n, P* out, K launch) {
     CTX_GUARD_HOST(c);
     if (n == 0) return BN_OK;
     if (!p || !k || !out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
@@ -473,7 +507,7 @@ static int host_mul(bn_ctx* c, const P* p, const bn_fr* k, size_t n, P* out, K k
     bn_fr* dk = (bn_fr*)(dout + n);
     HIPCHK(c, hipMemcpyAsync(dp, p, n * sizeof(P), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(dk, k, n * sizeof(bn_fr), hipMemcpyHostToDevice, c->stream));
-    kernel<<<grid_for(n), kBlock, 0, c->stream>>>(dp, dk, n, dout);
+    launch(dp, dk, n, dout, c->stream);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemcpyAsync(out, dout, n * sizeof(P), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -656,7 +690,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             const SegPlan plan = seg_plan(m);
             RET_IF(prepare(c, d_p + off, d_q + off, m, 0, s));
             mark(1);
-            k_miller_seg<<<grid_for(kPathLanes * plan.S * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
+            k_miller_seg<<<grid_pair(kPathLanes * plan.S * m), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
                                                                                slot_region(c, kRegionSeg));
             mark(2);
             k_horner_wide<<<grid_for(16 * m), kBlock, 0, s>>>(slot_region(c, kRegionSeg), m, plan, 1, d_out + off,
@@ -672,12 +706,12 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
                                                                         c->slots);
             mark(1);
         } else {
-            k_prepare<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags,
+            k_prepare<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags,
                                                                   c->d_err, 0);
             mark(1);
             if (c->miller_form == 2) {  // the segment kernel with one segment: the whole loop
                 const SegPlan whole = seg_plan(~(size_t)0 >> 1);
-                k_miller_seg<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, whole,
+                k_miller_seg<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, whole,
                                                                           c->slots);
             } else {
                 k_miller<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, c->slots);
@@ -829,7 +863,7 @@ static int batch_host(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, int m
     RET_IF(clear_err(c, c->stream));
     const size_t nchunks = (n + kChunk - 1) / kChunk;
     const size_t m0 = n < kChunk ? n : kChunk;
-    const SegPlan plan = seg_plan(m0);
+    const SegPlan plan = batch_plan(m0);
     RET_IF(reserve(c, m0));
     if (nchunks * plan.S > c->cap) return fail(c, BN_ERR_INVALID_ARGUMENT, "too many chunks");
     uint32_t* parts = parts_region(c, nchunks);
@@ -1027,7 +1061,7 @@ int bn_g1_mul_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_fr* d_k, size_t n, 
     CTX_GUARD(c);
     if (n == 0) return BN_OK;
     if (!d_p || !d_k || !d_out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
-    k_g1_mul<<<grid_for(n), kBlock, 0, pick(c, stream)>>>(d_p, d_k, n, d_out);
+    g1_mul_launch(d_p, d_k, n, d_out, pick(c, stream));
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
@@ -1041,11 +1075,11 @@ int bn_g2_mul_many_dev(bn_ctx* c, const bn_g2* d_p, const bn_fr* d_k, size_t n, 
 }
 int bn_g1_mul_many(bn_ctx* c, const bn_g1* p, const bn_fr* k, size_t n, bn_g1* out) {
     if (c && !c->subs.empty()) return bn_multi_g1_mul_many(c, p, k, n, out);
-    return host_mul(c, p, k, n, out, k_g1_mul);
+    return host_mul(c, p, k, n, out, g1_mul_launch);
 }
 int bn_g2_mul_many(bn_ctx* c, const bn_g2* p, const bn_fr* k, size_t n, bn_g2* out) {
     if (c && !c->subs.empty()) return bn_multi_g2_mul_many(c, p, k, n, out);
-    return host_mul(c, p, k, n, out, k_g2_mul);
+    return host_mul(c, p, k, n, out, g2_mul_launch);
 }
 
 int bn_fq12_op_many(bn_ctx* c, int op, const bn_gt* a, const bn_gt* b, size_t n, bn_gt* out) {
@@ -1210,7 +1244,7 @@ int bn_gt_pow_many_dev(bn_ctx* c, const bn_gt* d_a, const bn_fr* d_k, size_t n, 
     WsUse use{c, s};
     for (size_t off = 0; off < n; off += kChunk) {
         const size_t m = (n - off) < kChunk ? (n - off) : kChunk;
-        k_gt_pow<<<grid_for(kPathLanes * m), kBlock, 0, s>>>(d_a + off, d_k + off, m, d_out + off, c->slots);
+        k_gt_pow<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(d_a + off, d_k + off, m, d_out + off, c->slots);
         HIPCHK(c, hipGetLastError());
     }
     return BN_OK;
@@ -1220,7 +1254,7 @@ int bn_gt_pow_many(bn_ctx* c, const bn_gt* a, const bn_fr* k, size_t n, bn_gt* o
     return staged(c, n, {{a, sizeof(bn_gt)}, {k, sizeof(bn_fr)}}, {{out, sizeof(bn_gt)}},
                   [&](void** d, size_t m, hipStream_t s) -> int {
                       RET_IF(reserve(c, m));
-                      k_gt_pow<<<grid_for(kPathLanes * m), kBlock, 0, s>>>((const bn_gt*)d[0], (const bn_fr*)d[1], m, (bn_gt*)d[2],
+                      k_gt_pow<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>((const bn_gt*)d[0], (const bn_fr*)d[1], m, (bn_gt*)d[2],
                                                                          c->slots);
                       return BN_OK;
                   });

@@ -171,20 +171,101 @@ BN_INLINE Jac<F> jac_neg(const Jac<F>& a) {
     return {a.x, F_select(z, a.y, F_neg(a.y)), a.z};
 }
 
-// MSB-first double-and-add over the 256 bits of the canonical scalar
-// (mod.rs:272-292).  The bit pattern differs per lane: both steps are computed
-// and selected, so every lane follows exactly the reference's chain and the
-// Jacobian output is bit-identical.
-template <template <int> class F>
-BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8]) {
+// MSB-first double-and-add over the bits of the canonical scalar
+// (mod.rs:272-292): for every bit below the top set one, a doubling, then an
+// addition of p when the bit is set.  Every lane follows exactly the
+// reference's chain, so the Jacobian output is bit-identical.
+//
+// The chains differ per lane, so a wave schedules them (BN_MUL_SCHED = 1): each
+// iteration runs ONE kind of step -- the addition for the lanes whose next step
+// is an addition, or the doubling for those whose next step is a doubling --
+// chosen by a ballot: the addition once at least 3/5 of the unfinished lanes
+// wait for it (or no lane waits for a doubling).  A lane's own steps keep their
+// order, so its result is unchanged; lanes simply drift apart within the wave.
+// Lockstep execution (BN_MUL_SCHED = 0: every bit runs the doubling and the
+// masked addition on every lane) executes 253 x (7 + 16) Fq-mul per lane for
+// random scalars; the scheduled chain ~8 % less (a simulation of 64 random
+// 254-bit scalars: 5,302 against 5,819 Fq-mul-weighted steps).
+#ifndef BN_MUL_SCHED
+#define BN_MUL_SCHED 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BN_BALLOT_COUNT(p) ((uint32_t)__popcll(__ballot((int)(p))))
+#else
+#define BN_BALLOT_COUNT(p) ((uint32_t)((p) ? 1 : 0))
+#endif
+// `step(t)` runs at the start of step t (the kernels' issue balance, kernels.h)
+struct NoBitStep {
+    BN_INLINE void operator()(int) const {}
+};
+template <template <int> class F, typename Step = NoBitStep>
+BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8], Step&& step = Step{}) {
     Jac<F> res = jac_zero<F>();
-    bool found_one = false;
     const bool p_zero = jac_is_zero(p);
+#if BN_MUL_SCHED
+    // lane state: `w` holds the scalar shifted so that the next bit to consume is
+    // bit 31 of w[7]; `left` = bits still to consume after the top set bit;
+    // `need_add`: the lane's next step is the addition of the current bit
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = k[i];
+    // top set bit: shift it out (its addition is pending), count the bits below it
+    int top = -1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (w[i]) top = 32 * i + 31 - __builtin_clz(w[i]);
+    bool need_add = top >= 0;  // zero + p: the reference's first addition (found_one)
+    int left = top;            // bits below the top one
+    {
+        // left-align: shift by 255 - top + 1 so the bit below the top is bit 31 of w[7]
+        const int sh = top >= 0 ? 256 - top : 0;  // 1..256
+        const int ws = sh >> 5, bs = sh & 31;
+        uint32_t t[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {  // t[i] = (w << sh) word i, from words i - ws and i - ws - 1
+                const uint32_t hi = (i - j == ws) ? w[j] : 0u;
+                const uint32_t lo = (i - j == ws + 1) ? w[j] : 0u;
+                v |= (bs ? (hi << bs) | (lo >> (32 - bs)) : hi);
+            }
+            t[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = t[i];
+    }
+    int it = 0;
+#pragma unroll 1
+    for (;;) {
+        const bool need_dbl = !need_add && left > 0;
+        const uint32_t n_add = BN_BALLOT_COUNT(need_add), n_dbl = BN_BALLOT_COUNT(need_dbl);
+        if (n_add + n_dbl == 0) break;  // wave-uniform
+        step(it++);
+        if (n_dbl == 0 || 5 * n_add >= 3 * (n_add + n_dbl)) {
+            Jac<F> a = jac_add(res, p, p_zero);
+            res = {F_select(need_add, a.x, res.x), F_select(need_add, a.y, res.y), F_select(need_add, a.z, res.z)};
+            need_add = false;
+        } else {
+            Jac<F> d = jac_double(res);
+            res = {F_select(need_dbl, d.x, res.x), F_select(need_dbl, d.y, res.y), F_select(need_dbl, d.z, res.z)};
+            // the doubling consumed the next bit: its addition is pending when it is set
+            const bool b = (w[7] >> 31) != 0;
+            need_add = need_dbl ? b : need_add;
+            left -= need_dbl ? 1 : 0;
+#pragma unroll
+            for (int i = 7; i > 0; --i) w[i] = need_dbl ? (w[i] << 1) | (w[i - 1] >> 31) : w[i];
+            w[0] = need_dbl ? w[0] << 1 : w[0];
+        }
+    }
+#else
+    bool found_one = false;
     uint32_t w[8];  // scalar, shifted left one bit per step (no indexed private arrays)
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = k[i];
 #pragma unroll 1
     for (int bit = 255; bit >= 0; --bit) {
+        step(255 - bit);
         const bool b = w[7] >> 31;
 #pragma unroll
         for (int i = 7; i > 0; --i) w[i] = (w[i] << 1) | (w[i - 1] >> 31);
@@ -199,6 +280,7 @@ BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8]) {
             found_one = found_one || b;
         }
     }
+#endif
     return res;
 }
 

@@ -48,6 +48,30 @@ BN_INLINE Fq<B> fq_partner(const Fq<B>& a) {
     for (int l = 0; l < 9; ++l) r.v[l] = swap_pair(a.v[l]);
     return r;
 }
+// coordinate c0 (CTRL 0xA0: quad_perm [0,0,2,2]) or c1 (0xF5: [1,1,3,3]) of the
+// element on both lanes of the pair: one DPP move per digit, no select
+template <int CTRL>
+BN_INLINE uint32_t bcast_pair(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+#else
+    return v;  // host builds run one lane per element: see the host forms below
+#endif
+}
+template <int B>
+BN_INLINE Fq<B> fq_bcast_c0(const Fq<B>& a) {
+    Fq<B> r;
+#pragma unroll
+    for (int l = 0; l < 9; ++l) r.v[l] = bcast_pair<0xA0>(a.v[l]);
+    return r;
+}
+template <int B>
+BN_INLINE Fq<B> fq_bcast_c1(const Fq<B>& a) {
+    Fq<B> r;
+#pragma unroll
+    for (int l = 0; l < 9; ++l) r.v[l] = bcast_pair<0xF5>(a.v[l]);
+    return r;
+}
 template <int K>
 BN_INLINE Fq2<K> wrap2(const Fq<K>& x) { return {x}; }
 
@@ -95,6 +119,11 @@ BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) {
 }
 #ifndef BN_FQ2_FENCE
 #define BN_FQ2_FENCE 1
+#endif
+// 1: the split Fq2 product takes its operand's c0 / c1 on both lanes by DPP
+// broadcast (quad_perm) instead of a partner swap plus a per-lane select
+#ifndef BN_FQ2_BCAST
+#define BN_FQ2_BCAST 1
 #endif
 template <int B>
 BN_INLINE void fq2_fence(Fq2<B>& a) {
@@ -174,9 +203,16 @@ BN_INLINE auto fq2_mul_split(const Fq2<A>& a, const Fq2<B>& b) {
     } else {
         const bool odd = lane_odd();
         const Fq<A> pa = fq_partner(a.c);
+#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_BCAST
+        // y = b0 and c1 = b1 on both lanes straight from DPP (no select for y)
+        const Fq<B> y = fq_bcast_c0(b.c);
+        const Fq<B> c1 = fq_bcast_c1(b.c);
+        const auto w = fq_pick(odd, c1, fq_neg_lazy(c1));
+#else
         const Fq<B> pb = fq_partner(b.c);
         const Fq<B> y = fq_select(odd, pb, b.c);
         const auto w = fq_pick(odd, b.c, fq_neg_lazy(pb));
+#endif
         return wrap2(fq_dot2(a.c, y, pa, w));
     }
 }

@@ -384,20 +384,21 @@ __device__ __forceinline__ void fr_to_canonical(const bn_fr& k, uint32_t out[8])
 
 __device__ __forceinline__ size_t lane_id() { return (size_t)blockIdx.x * blockDim.x + threadIdx.x; }
 
-// ---------------------------------------------------------------- two-wave issue balance
-// The throughput kernels (k_pairing_fused, k_fq12_vm) run exactly two waves per
-// SIMD, both issue-bound on VALU.  The SIMD arbitrates VALU issue between them by
-// priority, then age (MI355X_MICROARCH.md, "Two waves per SIMD"), so at equal
-// priority the older wave runs ahead and the younger one finishes its second half
-// ALONE, at the lone-wave issue rate: the measured average wave lifetime was
-// ~0.77 of the kernel (profiles/pmc_summary.json).
-// Balance: these kernels launch kPairBlock = 512 threads, i.e. one workgroup of
-// eight waves per CU holding both waves of each SIMD.  Each wave publishes its
-// program position in LDS at every step of its main loop and raises its priority
-// (s_setprio 1) while it is not ahead of the other wave on its SIMD (found from
-// HW_ID's SIMD field at start), else drops to 0 -- so the two waves alternate the
-// lead and finish together.  Scheduling only: no value depends on it.
-// BN_BALANCE=0 builds the plain form (A/B).
+// ---------------------------------------------------------------- issue balance
+// The throughput kernels run several identical, VALU-issue-bound waves per SIMD
+// (k_pairing_fused, k_fq12_vm, k_gt_pow, k_miller_seg, k_g1_mul: two).  The SIMD arbitrates VALU issue between them by priority, then age
+// (MI355X_MICROARCH.md, "Two waves per SIMD"), so at equal priority the older
+// wave runs ahead and the younger one finishes ALONE, at the lone-wave issue
+// rate: the measured average wave lifetime was ~0.77 of the kernel
+// (profiles/pmc_summary.json).
+// Balance: such a kernel launches one workgroup holding every wave of its CU
+// (kPairBlock = 512 threads for two waves per SIMD; up to 1024 supported).  Each wave
+// publishes its program position in LDS at every step of its main loop and sets
+// its priority (s_setprio) to the number of waves on its SIMD (found from
+// HW_ID's SIMD field at start) that are AHEAD of it, so laggards issue first and
+// the waves finish together.  Scheduling only: no value depends on it.
+// BN_BALANCE=0 builds the plain form (A/B): 7.6 -> 8.3 M pairings/s
+// (profiles/r3a_ab_balance.txt).
 #ifndef BN_BALANCE
 #define BN_BALANCE 1
 #endif
@@ -405,12 +406,15 @@ __device__ __forceinline__ size_t lane_id() { return (size_t)blockIdx.x * blockD
 #define BN_PAIR_BLOCK 512
 #endif
 constexpr int kPairBlock = BN_PAIR_BLOCK;
+constexpr int kMaxBlock = 1024;
 struct Balance {
-    uint32_t w = 0, partner = 0;
+    uint32_t w = 0;        // this wave's index in the block
+    uint32_t partner = 0;  // the first other wave of the block on this wave's SIMD (itself if none)
+    uint32_t more = 0;     // any further ones (bit j = wave j): more than two waves per SIMD
 };
 #if BN_BALANCE && defined(__HIP_DEVICE_COMPILE__)
-__shared__ uint32_t g_bal_prog[kPairBlock / 64];
-__shared__ uint32_t g_bal_simd[kPairBlock / 64];
+__shared__ uint32_t g_bal_prog[kMaxBlock / 64];
+__shared__ uint32_t g_bal_simd[kMaxBlock / 64];
 // every thread of the block calls this (it has a barrier), before any early return
 __device__ __forceinline__ Balance balance_init() {
     Balance b;
@@ -421,21 +425,29 @@ __device__ __forceinline__ Balance balance_init() {
     g_bal_prog[b.w] = 0;
     __syncthreads();
     const uint32_t nw = blockDim.x >> 6;
-    b.partner = b.w;
+    uint32_t m = 0;
     for (uint32_t j = 0; j < nw; ++j)
-        if (j != b.w && g_bal_simd[j] == g_bal_simd[b.w]) b.partner = j;
-    b.partner = __builtin_amdgcn_readfirstlane(b.partner);
+        if (j != b.w && g_bal_simd[j] == g_bal_simd[b.w]) m |= 1u << j;
+    m = __builtin_amdgcn_readfirstlane(m);
+    b.partner = m ? (uint32_t)__builtin_ctz(m) : b.w;
+    b.more = m & (m - 1);
     return b;
 }
-// `pos`: this wave's position in the (shared) program, non-decreasing
+// `pos`: this wave's position in the (shared) program, non-decreasing.  The
+// priority is the number of other waves on the SIMD not behind this one (a tie
+// counts: two tied waves both run at 1, and age decides between them).
 __device__ __forceinline__ void balance_step(const Balance& b, uint32_t pos) {
     volatile uint32_t* pr = g_bal_prog;
     pr[b.w] = pos;
-    const uint32_t other = __builtin_amdgcn_readfirstlane(pr[b.partner]);
-    if (pos > other)
-        __builtin_amdgcn_s_setprio(0);
-    else
-        __builtin_amdgcn_s_setprio(1);
+    uint32_t ahead = __builtin_amdgcn_readfirstlane(pr[b.partner]) >= pos && b.partner != b.w ? 1u : 0u;
+    if (b.more) {
+        for (uint32_t m = b.more; m; m &= m - 1)
+            ahead += __builtin_amdgcn_readfirstlane(pr[__builtin_ctz(m)]) >= pos ? 1u : 0u;
+        if (ahead >= 3) __builtin_amdgcn_s_setprio(3);
+        else if (ahead == 2) __builtin_amdgcn_s_setprio(2);
+    }
+    if (ahead == 1) __builtin_amdgcn_s_setprio(1);
+    else if (ahead == 0) __builtin_amdgcn_s_setprio(0);
 }
 #else
 __device__ __forceinline__ Balance balance_init() { return Balance{}; }
@@ -487,13 +499,18 @@ inline void vm_step(uint32_t out[2], uint32_t op, uint32_t d, uint32_t a, uint32
 // Segments of the Miller loop's 64 NAF digits (k_miller_seg / k_horner_wide):
 // segment s covers digits [lo[s], hi[s]) and starts at line coefficient idx[s]
 constexpr int kMaxSeg = 16;
+// K: pairs per lane pair -- the reference's shared-squaring multi-Miller loop
+// (mod.rs:609-640): lane pair g of a segment squares its accumulator once per
+// digit and multiplies in the lines of pairs g, g + G, ..., g + (K-1) G
+// (G = ceil(n / K)); K = 1 for pairing_many's per-pair loops
 struct SegPlan {
     int S;
+    int K;
     int lo[kMaxSeg], hi[kMaxSeg], idx[kMaxSeg];
 };
 
 // ---------------------------------------------------------------- kernels
-__global__ void __launch_bounds__(kBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
+__global__ void __launch_bounds__(kPairBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
                                                        const uint32_t* __restrict__ paff,
                                                        const uint8_t* __restrict__ flags, size_t n, SegPlan plan,
                                                        uint32_t* __restrict__ out);
@@ -502,13 +519,13 @@ __global__ void __launch_bounds__(kBlock) k_miller_seg(const uint32_t* __restric
 // exponentiation when do_fe
 __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, size_t n, SegPlan plan,
                                                         int do_fe, bn_gt* __restrict__ out, int* __restrict__ err);
-__global__ void __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
+__global__ void __launch_bounds__(kPairBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
                           uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
                           int* __restrict__ err, int mode);
 // the same outputs on kPrepareWideLanes lanes per pair (kernels_pairing.hip): four
 // lane pairs run each line step's independent products side by side
 constexpr int kPrepareWideLanes = 8;
-__global__ void __launch_bounds__(kBlock) k_prepare_wide(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
+__global__ void __launch_bounds__(kPairBlock) k_prepare_wide(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
                                                          size_t n, uint32_t* __restrict__ coeffs,
                                                          uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
                                                          int* __restrict__ err, int mode);
@@ -532,9 +549,9 @@ __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __r
 __global__ void __launch_bounds__(kBlock) k_err_status(const int* __restrict__ err, int* __restrict__ status);
 __global__ void __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g, size_t n, uint32_t* __restrict__ f);
 __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict__ f, size_t n, size_t stride, bn_gt* __restrict__ g);
-__global__ void __launch_bounds__(kBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g1* __restrict__ out);
+__global__ void __launch_bounds__(kPairBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g1* __restrict__ out);
 __global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g2* __restrict__ out);
-__global__ void __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a, const bn_fr* __restrict__ k, size_t n,
+__global__ void __launch_bounds__(kPairBlock) k_gt_pow(const bn_gt* __restrict__ a, const bn_fr* __restrict__ k, size_t n,
                                                    bn_gt* __restrict__ out, uint32_t* __restrict__ ws);
 // kernels_codec.hip (codec.h): encodings, square roots, validation, decompression
 __global__ void __launch_bounds__(kBlock) k_fq_from_slice(const uint8_t* __restrict__ be, size_t n, bn_fq* __restrict__ out, uint8_t* __restrict__ st);

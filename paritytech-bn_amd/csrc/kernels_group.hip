@@ -9,15 +9,20 @@
 namespace bn {
 
 // ---------------------------------------------------------------- scalar multiplication
-__global__ void __launch_bounds__(kBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n,
-                                                   bn_g1* __restrict__ out) {
+// Launched with kPairBlock threads per block when the batch gives every CU a
+// whole block (kG1MulPairBlockMin, capi.hip), else kBlock: the issue balance of
+// kernels.h between the two waves each SIMD then holds.  (1024-thread blocks,
+// four waves per SIMD, cap the kernel at 128 VGPRs: 428 B of spills.)
+__global__ void __launch_bounds__(kPairBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n,
+                                                     bn_g1* __restrict__ out) {
     fold_table_init();
+    const Balance bal = balance_init();
     const size_t i = lane_id();
     if (i >= n) return;
     uint32_t s[8];
     fr_to_canonical(k[i], s);
     G1J a = {widen<kPt>(ld_ref(p[i].x)), widen<kPt>(ld_ref(p[i].y)), widen<kPt>(ld_ref(p[i].z))};
-    G1J r = jac_mul(a, s);
+    G1J r = jac_mul(a, s, [&](int t) { balance_step(bal, (uint32_t)t); });
     st_ref(out[i].x, r.x);
     st_ref(out[i].y, r.y);
     st_ref(out[i].z, r.z);

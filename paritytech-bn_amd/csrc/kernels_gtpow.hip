@@ -45,10 +45,13 @@ __device__ __forceinline__ bool gt_pow_wave_cyclotomic(const Fq12<kF>& x) {
     return __all(member);
 }
 
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __restrict__ a,
-                                                               const bn_fr* __restrict__ k, size_t n,
-                                                               bn_gt* __restrict__ out, uint32_t* __restrict__ ws) {
+// Launched with kPairBlock threads per block (kernels.h: issue balance; program
+// position = table entry, then 16 + 5 * window + squaring).
+__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_gt_pow(const bn_gt* __restrict__ a,
+                                                                   const bn_fr* __restrict__ k, size_t n,
+                                                                   bn_gt* __restrict__ out, uint32_t* __restrict__ ws) {
     fold_table_init();
+    const Balance bal = balance_init();
     const size_t l = lane_id(), i = l / kL;
     if (i >= n) return;
     // slot access through a buffer descriptor with the lane stride laundered per
@@ -70,6 +73,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __r
     Fq12<kF> t = x;
 #pragma unroll 1
     for (uint32_t j = 2; j < 16; ++j) {
+        balance_step(bal, j);
         const size_t nn = stride();
         t = mul12(t, ld_fq12_buf<kF>(slot(1, nn), nn, l));
         st_fq12_buf(slot(j, nn), nn, l, t);
@@ -93,6 +97,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_gt_pow(const bn_gt* __r
             e[0] <<= 4;
 #pragma unroll 1
             for (int s = 0; s < 4; ++s) {
+                balance_step(bal, 16u + 5u * (uint32_t)(62 - w) + (uint32_t)s);
                 if constexpr (decltype(cyc)::value) acc = cyc_sqr(acc);
                 else acc = narrow12<kF>(fq12_sqr(acc));
             }

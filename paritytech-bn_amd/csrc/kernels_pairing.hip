@@ -75,18 +75,23 @@ __device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p
     return a;
 }
 
-// to_affine + the 87 line coefficients (AffineG2::precompute) -> HBM
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
-                                                                size_t n, uint32_t* __restrict__ coeffs,
-                                                                uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
-                                                                int* __restrict__ err, int mode) {
+// to_affine + the 87 line coefficients (AffineG2::precompute) -> HBM.
+// Launched with kPairBlock threads per block (kernels.h: issue balance).
+__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_prepare(const bn_g1* __restrict__ p,
+                                                                    const bn_g2* __restrict__ q, size_t n,
+                                                                    uint32_t* __restrict__ coeffs,
+                                                                    uint32_t* __restrict__ paff,
+                                                                    uint8_t* __restrict__ flags,
+                                                                    int* __restrict__ err, int mode) {
     fold_table_init();
+    const Balance bal = balance_init();
     const size_t l = lane_id(), i = l / kL, nl = kL * n;
     if (i >= n) return;
     const PairAffine a = pair_to_affine(p, q, i, l, flags, err, mode);
     st_fq(paff, nl, l, 0, a.px);
     st_fq(paff, nl, l, 1, a.py);
     g2_precompute(a.qa, [&](int k, const Ell& e) {
+        balance_step(bal, (uint32_t)k);
         st_fq2(coeffs, nl, l, k * 6 + 0, e.ell_0);
         st_fq2(coeffs, nl, l, k * 6 + 2, e.ell_vw);
         st_fq2(coeffs, nl, l, k * 6 + 4, e.ell_vv);
@@ -190,13 +195,15 @@ __device__ __forceinline__ Ell pw_mixed_addition_step(G2Proj& s, const G2Aff<BB>
     return {narrow<kLine>(l0), narrow<kLine>(d), narrow<kLine>(fq2_neg(e))};
 }
 
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare_wide(const bn_g1* __restrict__ p,
-                                                                     const bn_g2* __restrict__ q, size_t n,
-                                                                     uint32_t* __restrict__ coeffs,
-                                                                     uint32_t* __restrict__ paff,
-                                                                     uint8_t* __restrict__ flags,
-                                                                     int* __restrict__ err, int mode) {
+// Launched with kPairBlock threads per block (kernels.h: issue balance).
+__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_prepare_wide(const bn_g1* __restrict__ p,
+                                                                         const bn_g2* __restrict__ q, size_t n,
+                                                                         uint32_t* __restrict__ coeffs,
+                                                                         uint32_t* __restrict__ paff,
+                                                                         uint8_t* __restrict__ flags,
+                                                                         int* __restrict__ err, int mode) {
     fold_table_init();
+    const Balance bal = balance_init();
     const size_t l = lane_id(), i = l / kPW, nl = kL * n;
     if (i >= n) return;
     const size_t lt = i * kL + (l & 1);  // this lane's index in k_prepare's per-pair arrays
@@ -221,6 +228,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_prepare_wide(const bn_g
     int c = 0;
 #pragma unroll 1
     for (int d = 0; d < BN_NAF_DIGITS; ++d) {
+        balance_step(bal, (uint32_t)d);
         emit(c++, pw_doubling_step(r, k));
         if ((kNafNonzero >> d) & 1u) {
             const bool minus = (kNafMinus >> d) & 1u;
@@ -286,28 +294,75 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* 
     st_fq12(f_out, nl, l, f);
 }
 
-// Miller loop in segments (pairing_batch / miller_loop_batch with fewer pairs
-// than fill the GPU): lane pair (segment s, pair i) -- segment-major, so a wave
-// reads consecutive pairs' coefficients -- computes pair i's loop over the
-// segment's digits (pairing.h miller_segment) into element s * n + i of `out`
-// (split layout, stride S * n).  Segment values of a pair with a zero point are one.
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
-                                                                   const uint32_t* __restrict__ paff,
-                                                                   const uint8_t* __restrict__ flags, size_t n,
-                                                                   SegPlan plan, uint32_t* __restrict__ out) {
+// Miller loop in segments (pairing_batch / miller_loop_batch, and small
+// pairing_many batches): lane pair (segment s, group g) -- segment-major, so a
+// wave reads consecutive pairs' coefficients -- runs the segment's digits
+// [lo, hi) of the loop from f = one for the K pairs g, g + G, ..., g + (K-1) G
+// (G = ceil(n / K)): per digit ONE squaring of the shared accumulator and the
+// line of every pair (mod.rs:609-640's shared-squaring loop; squaring is a ring
+// homomorphism and Fq12 is commutative, so the product over groups and the
+// Horner recombination over segments give exactly miller_loop_batch's value).
+// The result goes to element s * G + g of `out` (split layout, stride S * G).
+// A pair with a zero point (flags) or past n contributes the line one
+// (ell_0 = 1, ell_vw = ell_vv = 0): the sparse product by it is f itself.
+// Launched with kPairBlock threads per block (kernels.h: issue balance).
+__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
+                                                                       const uint32_t* __restrict__ paff,
+                                                                       const uint8_t* __restrict__ flags, size_t n,
+                                                                       SegPlan plan, uint32_t* __restrict__ out) {
     fold_table_init();
-    const size_t l = lane_id(), pr = l / kL, nl = kL * n;
-    if (pr >= (size_t)plan.S * n) return;
-    const int s = (int)(pr / n);
-    const size_t lt = (pr % n) * kL + (l % kL);  // the pair's lane in the per-pair arrays
-    const Fq<2> px = ld_fq<2>(paff, nl, lt, 0);
-    const Fq<2> py = ld_fq<2>(paff, nl, lt, 1);
-    Fq12<kF> f = miller_segment(px, py, plan.lo[s], plan.hi[s], plan.idx[s], [&](int k) {
-        return Ell{ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 0), ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 2),
-                   ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 4)};
-    });
-    if (flags[lt]) f = widen<kF>(fq12_one());
-    st_fq12(out, kL * plan.S * n, l, f);
+    const Balance bal = balance_init();
+    const size_t l = lane_id(), lp = l / kL, nl = kL * n;
+    const size_t K = (size_t)plan.K, G = (n + K - 1) / K;
+    if (lp >= (size_t)plan.S * G) return;
+    const int s = (int)(lp / G);
+    const size_t g = lp % G, c = l % kL;
+    const Ell one_line = {widen<kLine>(fq2_one()), widen<kLine>(fq2_zero()), widen<kLine>(fq2_zero())};
+    // line k of pair t of this group, with the pair's affine P
+    struct PairLine {
+        Ell e;
+        Fq<2> px, py;
+    };
+    auto pair_line = [&](size_t t, int k) {
+        const size_t j = g + t * G;
+        const bool live = j < n && !flags[j * kL + c];
+        const size_t lt = (j < n ? j : 0) * kL + c;  // the pair's lane in the per-pair arrays
+        PairLine r;
+        mem_fence();  // load right before use: K pairs' lines are never held at once
+        r.e = Ell{ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 0), ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 2),
+                  ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 4)};
+        r.px = ld_fq<2>(paff, nl, lt, 0);
+        r.py = ld_fq<2>(paff, nl, lt, 1);
+        if (!live) r.e = one_line;
+        return r;
+    };
+    // Digits lo..hi-1, then (last segment) the two closing lines as pseudo-digits
+    // 64 and 65 without a squaring; per digit one squaring (none at lo: f starts
+    // at one, so the first line is f itself) and one or two passes over the K
+    // pairs' lines.  One copy of the squaring and of the sparse product.
+    const int lo = plan.lo[s], hi = plan.hi[s];
+    const int end = hi == BN_NAF_DIGITS ? BN_NAF_DIGITS + 2 : hi;
+    int idx = plan.idx[s];
+    Fq12<kF> f = widen<kF>(fq12_one());
+#pragma unroll 1
+    for (int i = lo; i < end; ++i) {
+        balance_step(bal, (uint32_t)(i - lo));
+        const bool closing = i >= BN_NAF_DIGITS;
+        if (!closing && i > lo) f = narrow12<kF>(fq12_sqr(f));
+        const int passes = closing ? 1 : 1 + (int)((kNafNonzero >> i) & 1u);
+#pragma unroll 1
+        for (int ps = 0; ps < passes; ++ps, ++idx) {
+#pragma unroll 1
+            for (size_t t = 0; t < K; ++t) {
+                const PairLine pl = pair_line(t, idx);
+                if (i == lo && ps == 0 && t == 0)
+                    f = line_from_one(pl.e, pl.px, pl.py);  // one * line (mod.rs:589 on f = one)
+                else
+                    f = apply_line(f, pl.e, pl.px, pl.py);
+            }
+        }
+    }
+    st_fq12(out, kL * plan.S * G, l, f);
 }
 
 }  // namespace bn

@@ -69,9 +69,14 @@ struct LineOps {
 template <int X>
 BN_INLINE LineOps line_ops(const Fq2<X>& v_in) {
     const Fq<kv(X)> v = fq_norm(v_in.c);
-    const Fq<kv(X)> pv = fq_partner(v);
     const bool odd = lane_odd();
+#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_BCAST
+    const Fq<kv(X)> c1 = fq_bcast_c1(v);
+    return {widen<kLine>(fq_bcast_c0(v)), widen<8>(fq_norm(fq_pick(odd, c1, fq_neg_lazy(c1))))};
+#else
+    const Fq<kv(X)> pv = fq_partner(v);
     return {widen<kLine>(fq_select(odd, pv, v)), widen<8>(fq_norm(fq_pick(odd, v, fq_neg_lazy(pv))))};
+#endif
 }
 // t += u * v for this lane's coordinate (u: f side, normalized)
 BN_INLINE void acc_mad2(Acc& t, const Fq<2>& u, const LineOps& v) {
@@ -212,11 +217,13 @@ BN_INLINE Fq12<kF> miller_fused(const G2Aff<B>& q, const Fq<PB>& px, const Fq<PB
 // [0, 64) in segments g_0 .. g_(S-1) gives f = (..((g_0)^(2^len_1) g_1)^(2^len_2)
 // ..) g_(S-1): squaring is a ring homomorphism, so the Horner recombination
 // (kernels_wide.hip k_horner_wide) reproduces mod.rs:579-640 exactly.
-template <int PB, typename Line>
-BN_INLINE Fq12<kF> miller_segment(const Fq<PB>& px, const Fq<PB>& py, int lo, int hi, int idx, Line&& line) {
+template <int PB, typename Line, typename Step = NoStep>
+BN_INLINE Fq12<kF> miller_segment(const Fq<PB>& px, const Fq<PB>& py, int lo, int hi, int idx, Line&& line,
+                                  Step&& step = Step{}) {
     Fq12<kF> f = widen<kF>(fq12_one());
 #pragma unroll 1
     for (int i = lo; i < hi; ++i) {
+        step(i - lo);
         f = sqr_line(f, i == lo, line(idx++), px, py);
         if ((kNafNonzero >> i) & 1u) f = apply_line(f, line(idx++), px, py);
     }

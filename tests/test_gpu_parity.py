@@ -17,6 +17,17 @@ def ctx():
 
 
 @pytest.fixture(scope="module")
+def ctx_tp():
+    """A context whose every pairing_many batch takes the THROUGHPUT path
+    (k_pairing_fused + k_fq12_vm + k_fe_out, the kernels bench.py's `value`
+    measures): the latency-path threshold is 0."""
+    from substrate_bn import Context
+    c = Context(0)
+    c.set_fe_wide_max(0)
+    return c
+
+
+@pytest.fixture(scope="module")
 def pairs():
     p, q, s, t = O.random_pairs(256, seed=1234, nthreads=NT)
     return p, q
@@ -216,3 +227,53 @@ def test_config3_g1_mul_full_size(ctx):
     base = ctx.g1_mul_many(np.tile(O.g1_one(), (n, 1)), np.roll(S, 7, axis=0))  # random Jacobian bases (z != 1)
     got = ctx.g1_mul_many(base, S)
     assert np.array_equal(got, O.g1_mul(base, S, NT))
+
+
+# ---- the throughput path (the kernels `value` measures) on the edge cases, vs the oracle
+def test_throughput_path_pairing_many(ctx_tp, pairs):
+    p, q = pairs
+    assert np.array_equal(ctx_tp.pairing_many(p, q), O.pairing_many(p, q, NT))
+
+
+def test_throughput_path_zero_points(ctx_tp, pairs):
+    """pairing() of a zero point is Fq12::one() (mod.rs:896), on k_pairing_fused / k_fe_out."""
+    p, q = pairs
+    p2, q2 = p[:4].copy(), q[:4].copy()
+    one = O.canon_to_mont_array([1])
+    p2[1] = 0
+    p2[1, 4:8] = one                 # G1::zero()
+    q2[2] = 0
+    q2[2, 8:12] = one                # G2::zero(): y = (1, 0)
+    assert np.array_equal(ctx_tp.pairing_many(p2, q2), O.pairing_many(p2, q2))
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 129, 255, 257, 511, 513])
+def test_throughput_path_ragged(ctx_tp, pairs, n):
+    """Sizes that leave partial waves and partial 512-thread blocks of the
+    balanced kernels, with zero points in the tail lanes (src/groups/mod.rs:894-902)."""
+    p, q = pairs
+    reps = (n + p.shape[0] - 1) // p.shape[0]
+    p2, q2 = np.tile(p, (reps, 1))[:n].copy(), np.tile(q, (reps, 1))[:n].copy()
+    one = O.canon_to_mont_array([1])
+    p2[n - 1] = 0
+    p2[n - 1, 4:8] = one             # G1::zero() in the last lane
+    if n > 2:
+        q2[n - 2] = 0
+        q2[n - 2, 8:12] = one        # G2::zero() in the lane before it
+    assert np.array_equal(ctx_tp.pairing_many(p2, q2), O.pairing_many(p2, q2, NT))
+
+
+def test_throughput_path_4096_and_final_exp(ctx_tp):
+    """4096 random pairings through the throughput kernels bit-exact against the
+    oracle; the step-machine final exponentiation alone on their Miller values,
+    a zero value included (fq12.rs:63-72 returns None)."""
+    p, q, _, _ = O.random_pairs(4096, seed=4097, nthreads=NT)
+    want = O.pairing_many(p, q, NT)
+    assert np.array_equal(ctx_tp.pairing_many(p, q), want)
+    f = ctx_tp.miller_loop_many(p[:300], q[:300])
+    f[7] = 0
+    fe, ok = ctx_tp.final_exponentiation_many(f)
+    assert ok[7] == 0 and not fe[7].any()
+    keep = np.ones(300, bool)
+    keep[7] = False
+    assert ok[keep].all() and np.array_equal(fe[keep], want[:300][keep])

@@ -106,6 +106,9 @@ for k, v in sorted(agg.items()):
                   "algorithmic_fqmul_per_element": alg, "elements_per_wave": per_wave,
                   "valu_lane_ops_per_algorithmic_mad": valu_per_mad,
                   "grbm_gui_active": m.get("GRBM_GUI_ACTIVE"),
+                  # average wave lifetime as a fraction of the kernel (GRBM_GUI_ACTIVE sums the 8 XCDs):
+                  # near 1 when the waves of a one-round launch finish together
+                  "wave_life_frac": cyc / (m["GRBM_GUI_ACTIVE"] / 8) if m.get("GRBM_GUI_ACTIVE") else None,
                   "note": "FETCH_SIZE corrected by the read factor calibrated on k_fe_out (known bytes), "
                           "WRITE_SIZE as counted (MI355X_MICROARCH §HBM); source %s" % tag}
     lines.append("%-16s %14.3e %14.3e %14.3e %12.3e %10.3f" % (k, fetch, write, valu, cyc, valu / cyc if cyc else 0))
