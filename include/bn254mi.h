@@ -205,6 +205,12 @@ int bn_set_phase_timing(bn_ctx* ctx, int enable);
  * $BN254MI_FE_WIDE_MAX; results are identical either way.  On a multi-device
  * context it applies to every device. */
 int bn_set_fe_wide_max(bn_ctx* ctx, size_t n);
+/* Within the latency path, bn_pairing_many_dev batches of at most n pairs run the
+ * whole pairing in ONE launch (k_pairing_latency: a wave computing the 87 lines of
+ * each pair feeds, through an LDS ring, 16-lane groups running the Miller loop and
+ * the final exponentiation); larger ones the segmented three-kernel form.
+ * Default 2048 or $BN254MI_LATENCY_MAX; 0 disables it; results are identical. */
+int bn_set_latency_max(bn_ctx* ctx, size_t n);
 /* device milliseconds per phase since the last read: ms[0] k_prepare (to_affine +
  * G2 lines), ms[1] k_miller, ms[2] final exponentiation (k_fq12_vm, or k_fe_wide for
  * batches up to the wide threshold), ms[3] k_fe_out (0 with k_fe_wide);

@@ -63,6 +63,10 @@ constexpr int kFeSlots = 32;  // slot 0: Miller value, 1: easy-part result, 2..:
 // throughput path: 8192 pairs 3.58 vs 5.43 ms, 16384 pairs 6.05 vs 5.43 ms
 // (profiles/r2j_latency_sweep.jsonl).  BN254MI_FE_WIDE_MAX or bn_set_fe_wide_max override.
 constexpr size_t kFeWideMaxDefault = 8192;
+// batches up to this size run the one-launch latency kernel (k_pairing_latency:
+// a line-producer wave feeding the wide Miller loop and final exponentiation);
+// BN254MI_LATENCY_MAX or bn_set_latency_max override (0: never)
+constexpr size_t kLatencyMaxDefault = 2048;  // crossover: 2048 pairs 1.27 vs 1.92 ms, 4096 2.46 vs 1.94 ms (profiles/r3e_latency.jsonl)
 // batches up to this size run k_prepare_wide (8 lanes per pair: 2^14 pairs fill
 // the GPU at two waves per SIMD).  BN254MI_PREPARE_WIDE_MAX overrides (0: never).
 constexpr size_t kPrepareWideMaxDefault = 16384;
@@ -439,9 +443,28 @@ int finish_product(bn_ctx* c, const SegPlan& plan, size_t nchunks, int do_fe, bn
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
+// The product of n <= c->latency_max device pairs: their Miller values from the
+// one-launch k_pairing_latency (no FE), the product reduction, then one group's
+// final exponentiation (do_fe: pairing_batch) or the Miller value itself
+// (miller_loop_batch) into *d_out
+int latency_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int mode, int do_fe, bn_gt* d_out,
+                    hipStream_t s) {
+    RET_IF(reserve(c, n));
+    k_pairing_latency<<<(unsigned)((n + kLatPairs - 1) / kLatPairs), kLatThreads, 0, s>>>(
+        d_p, d_q, n, nullptr, slot_region(c, kRegionSeg), mode, c->d_err);
+    HIPCHK(c, hipGetLastError());
+    RET_IF(product_wide(c, slot_region(c, kRegionSeg), n, n, n, 1, slot_region(c, kRegionResult), 1, 0, 1, s));
+    const SegPlan whole = cut_plan(1, 1);  // one segment: x = the product, then the FE when do_fe
+    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, whole, do_fe, d_out, c->d_err);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+bool use_latency_product(const bn_ctx* c, size_t n) { return n <= c->latency_max && n <= c->fe_wide_max; }
+
 // the whole product of n device pairs into *d_out; the caller holds the workspace
 int miller_product_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int mode, bn_gt* d_out,
                        hipStream_t s) {
+    if (use_latency_product(c, n)) return latency_product(c, d_p, d_q, n, mode, mode == 0, d_out, s);
     const size_t nchunks = (n + kChunk - 1) / kChunk;
     const size_t m0 = n < kChunk ? n : kChunk;
     const SegPlan plan = batch_plan(m0);
@@ -578,6 +601,8 @@ int bn_ctx_create(int device, bn_ctx** out) {
         const size_t v = (size_t)strtoull(e, nullptr, 10);
         if (v > 0 && v <= kChunk) c->host_piece = v;
     }
+    c->latency_max = kLatencyMaxDefault;
+    if (const char* e = getenv("BN254MI_LATENCY_MAX")) c->latency_max = (size_t)strtoull(e, nullptr, 10);
     c->prepare_wide_max = kPrepareWideMaxDefault;
     if (const char* e = getenv("BN254MI_PREPARE_WIDE_MAX")) c->prepare_wide_max = (size_t)strtoull(e, nullptr, 10);
     Prog P;
@@ -684,6 +709,19 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             if (c->timing && ev[k]) (void)hipEventRecord(ev[k], s);
         };
         mark(0);
+        if (m <= c->fe_wide_max && m <= c->latency_max) {
+            // the whole pairing in one launch: line producer + wide Miller loop and FE
+            // (kernels_wide.hip k_pairing_latency)
+            k_pairing_latency<<<(unsigned)((m + kLatPairs - 1) / kLatPairs), kLatThreads, 0, s>>>(
+                d_p + off, d_q + off, m, d_out + off, nullptr, 0, c->d_err);
+            mark(1);
+            mark(2);
+            mark(3);
+            mark(4);
+            HIPCHK(c, hipGetLastError());
+            if (c->timing) c->ev_marks.push_back(ev);
+            continue;
+        }
         if (m <= c->fe_wide_max) {
             // latency path: the Miller loop in segments on 2 * S lanes per pairing,
             // recombined and exponentiated on a 16-lane group per pairing
@@ -861,6 +899,21 @@ int bn_pairing_many(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, bn_gt* 
 // BN_ERR_TO_AFFINE / BN_ERR_FE_ZERO come from the device bits.
 static int batch_host(bn_ctx* c, const bn_g1* p, const bn_g2* q, size_t n, int mode, bool do_fe, bn_gt* out) {
     RET_IF(clear_err(c, c->stream));
+    if (use_latency_product(c, n)) {
+        RET_IF(stage(c, n * (sizeof(bn_g1) + sizeof(bn_g2)) + sizeof(bn_gt)));
+        bn_g1* dp = (bn_g1*)c->stage;
+        bn_g2* dq = (bn_g2*)(dp + n);
+        bn_gt* d = (bn_gt*)(dq + n);
+        HIPCHK(c, hipMemcpyAsync(dp, p, n * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(dq, q, n * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
+        RET_IF(latency_product(c, dp, dq, n, mode, do_fe ? 1 : 0, d, c->stream));
+        HIPCHK(c, hipMemcpyAsync(out, d, sizeof(bn_gt), hipMemcpyDeviceToHost, c->stream));
+        int bits = 0;
+        RET_IF(check_err(c, c->stream, &bits));
+        if (bits & (1 << BN_ERR_TO_AFFINE)) return fail(c, BN_ERR_TO_AFFINE, "ToAffineConversion");
+        if (bits & (1 << BN_ERR_FE_ZERO)) return fail(c, BN_ERR_FE_ZERO, "miller loop cannot produce zero");
+        return BN_OK;
+    }
     const size_t nchunks = (n + kChunk - 1) / kChunk;
     const size_t m0 = n < kChunk ? n : kChunk;
     const SegPlan plan = batch_plan(m0);
@@ -980,6 +1033,15 @@ int bn_miller_loop_batch_dev(bn_ctx* c, const bn_g2* d_q, const bn_g1* d_p, size
                              void* stream) {
     CTX_GUARD(c);
     return batch_dev(c, d_p, d_q, n, d_out, d_status, 1, pick(c, stream));
+}
+int bn_set_latency_max(bn_ctx* c, size_t n) {
+    if (c && !c->subs.empty()) {
+        for (bn_ctx* d : c->subs) RET_IF(bn_set_latency_max(d, n));
+        return BN_OK;
+    }
+    CTX_GUARD(c);
+    c->latency_max = n;
+    return BN_OK;
 }
 int bn_set_fe_wide_max(bn_ctx* c, size_t n) {
     if (c && !c->subs.empty()) {

@@ -40,6 +40,8 @@ struct bn_ctx {
     // coefficient traffic); 0 = k_prepare (line coefficients to HBM) + k_miller;
     // 2 = k_prepare + k_miller_seg with one segment
     int miller_form = 1;
+    // bn_pairing_many_dev batches of at most this many pairs run k_pairing_latency
+    size_t latency_max = 0;
     // batches of at most this many pairs take k_prepare_wide (8 lanes per pair)
     size_t prepare_wide_max = 0;
     int* d_err = nullptr;

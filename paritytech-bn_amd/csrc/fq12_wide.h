@@ -119,6 +119,57 @@ __device__ __noinline__ Fq<2> w12_mul(Fq<2> a, Fq<2> b) {
     return acc_redc<2>(t);
 }
 
+// Line ring of k_pairing_latency (kernels_wide.hip): per pair kLatRing lines of
+// x0, x4, x2, each stored as the three operand forms of the split product --
+// c0, c1 and -c1 (slots 3q, 3q + 1, 3q + 2; kWSlot words each) -- so a consumer
+// lane reads its two operands with no select or negation
+constexpr int kLatRing = 16;               // lines in flight per pair
+constexpr int kLatLineWords = 9 * kWSlot;  // words per line
+__shared__ uint32_t g_lat_ring[kLatPairs * kLatRing * kLatLineWords];  // 54 KB
+
+// a * line (fq12.rs:130-196, mul_by_024 on the w-basis): the line is
+// x0 + x4 w^3 + x2 w^4, its three Fq2 coefficients read from the ring at word
+// ln_off (an offset, so the compiler addresses LDS, not flat memory).  out_e = sum over the
+// three nonzero line coefficients b_m of a'_(e-m) * b_m with a'_i = xi * a_i
+// when the index wraps (w^6 = xi): six digit products per lane, one reduction.
+// The same residues as the reference's sparse product.
+__device__ __noinline__ Fq<2> w12_mul_line(Fq<2> a, uint32_t ln_off) {
+    const WL w = wl();
+    const uint32_t* ln = g_lat_ring + ln_off;
+    uint32_t* A_ = w.gb;
+    uint32_t* X_ = w.gb + kWArr;
+    w_put(A_, w.l, a);
+    w_put(X_, w.l, w_xi(a));
+    w_sync();
+    Acc t = {};
+    constexpr int kM[3] = {0, 3, 4};  // w-exponents of x0, x4, x2
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int m = kM[q];
+        const bool wrap = m > w.e;
+        const int i = wrap ? w.e - m + 6 : w.e - m;
+        const uint32_t* src = wrap ? X_ : A_;
+        const Fq<2> x0 = w_get<2>(src, 2 * i), x1 = w_get<2>(src, 2 * i + 1);
+        // line coordinates: normalized, value <= kLine p (the producer narrows them)
+        // c0: x0*b0 + x1*(-b1), c1: x0*b1 + x1*b0
+        const Fq<kLine> yo = w_get<kLine>(ln, 3 * q + w.c);
+        const Fq<kLine> yx = w_get<kLine>(ln, 3 * q + (w.c ? 0 : 2));
+        acc_mad(t, x0, yo);
+        acc_mad(t, x1, yx);
+    }
+    // value <= 6 * 2p * 4p: the reduction is below (48 p / 2^261 + 1) p < 2p
+    return acc_redc<2>(t);
+}
+// the line x0 + x4 w^3 + x2 w^4 itself as an element (one * line, the first
+// step of the loop from f = one)
+__device__ __forceinline__ Fq<2> w12_from_line(uint32_t ln_off) {
+    const WL w = wl();
+    const uint32_t* ln = g_lat_ring + ln_off;
+    const int q = w.e == 0 ? 0 : w.e == 3 ? 1 : 2;
+    const Fq<kLine> v = w_get<kLine>(ln, 3 * q + w.c);
+    return w_narrow(fq_select(w.e == 0 || w.e == 3 || w.e == 4, v, widen<kLine>(fq_zero())));
+}
+
 // Granger-Scott cyclotomic squaring (fq12.rs:198-247).  Pairs (z0,z1), (z2,z3),
 // (z4,z5) are the coefficient pairs (w^k, w^(k+3)), k = 0, 1, 2.  Lane pair e < 3
 // computes tmp_e = x*y for pair k = e; lane pair e >= 3 computes

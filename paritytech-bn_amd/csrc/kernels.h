@@ -546,6 +546,14 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
                                                              size_t n, size_t in_set, uint32_t* __restrict__ out,
                                                              size_t out_stride, size_t out_base, size_t out_set);
+// kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
+// (a producer wave for the lines, consumer groups for the wide Miller loop + FE)
+constexpr int kLatPairs = 8;
+constexpr int kLatThreads = 64 + kLatPairs * 16;  // 192: one producer wave, two consumer waves
+__global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __restrict__ p,
+                                                                 const bn_g2* __restrict__ q, size_t n,
+                                                                 bn_gt* __restrict__ out, uint32_t* __restrict__ f_out,
+                                                                 int mode, int* __restrict__ err);
 __global__ void __launch_bounds__(kBlock) k_err_status(const int* __restrict__ err, int* __restrict__ status);
 __global__ void __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g, size_t n, uint32_t* __restrict__ f);
 __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict__ f, size_t n, size_t stride, bn_gt* __restrict__ g);

@@ -10,6 +10,7 @@
 #include "fq.h"
 #define BN_SPLIT 1
 #include "fq12_wide.h"
+#include "lines_wide.h"
 
 namespace bn {
 
@@ -112,6 +113,148 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
         fq_store_ref(x, words);
     }
     if (w.l < 12) st_words(&out[e].c[w_gt_index(w)], words);
+}
+
+// ---------------------------------------------------------------- k_pairing_latency
+// pairing() of a few pairs in ONE launch, for latency (bn_pairing_many_dev
+// batches of at most kLatencyMaxDefault pairs, capi.hip).  A block holds
+// kLatPairs pairs and three waves:
+//  - wave 0, the producer: to_affine and the 87 line coefficients of each pair
+//    on eight lanes (lines_wide.h, as k_prepare_wide), each line scaled by P
+//    (ell_vw * Py, ell_vv * Px: mod.rs:589) and put into the pair's LDS ring;
+//  - waves 1-2, the consumers: one 16-lane group per pair runs the Miller loop
+//    on the wide layout (fq12_wide.h) right behind the producer -- per digit
+//    the generic square and the sparse product by each line as it arrives
+//    (mod.rs:579-607's order, so the Miller value is the reference's) -- then
+//    the final exponentiation (w12_final_exp), and stores the Gt image.
+// The loop needs no segments and no Horner recombination, and the three
+// kernels of the segmented latency path (k_prepare_wide, k_miller_seg,
+// k_horner_wide) become one.  Hand-off: the producer writes a line, waits for
+// its LDS writes (lgkmcnt(0)) and bumps the pair's `prod` counter; a consumer
+// spins (s_sleep) until `prod` passes the line it needs and bumps `cons` after
+// reading it; the producer keeps at most kLatRing lines ahead.  Both sides
+// always progress, so every wave reaches the end; the spins are capped anyway.
+// (the ring itself, g_lat_ring, is declared in fq12_wide.h beside w12_mul_line)
+__shared__ uint32_t g_lat_prod[kLatPairs], g_lat_cons[kLatPairs], g_lat_skip[kLatPairs];
+constexpr uint32_t kLatSpinCap = 1u << 26;  // ~4 s of s_sleep 1: never reached while both sides run
+
+// f_out != null (pairing_batch / miller_loop_batch): the Miller values go to
+// f_out (split layout, lane-strided, stride n; a zero-point pair's is one) for the
+// product reduction, and no final exponentiation runs here; mode 1
+// (miller_loop_batch) flags a zero point as BN_ERR_TO_AFFINE (lib.rs:629-630).
+__global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __restrict__ p,
+                                                                 const bn_g2* __restrict__ q, size_t n,
+                                                                 bn_gt* __restrict__ out, uint32_t* __restrict__ f_out,
+                                                                 int mode, int* __restrict__ err) {
+    fold_table_init();
+    if (threadIdx.x < kLatPairs) {
+        g_lat_prod[threadIdx.x] = 0;
+        g_lat_cons[threadIdx.x] = 0;
+        g_lat_skip[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    volatile uint32_t* prod = g_lat_prod;
+    volatile uint32_t* cons = g_lat_cons;
+    const size_t base = (size_t)blockIdx.x * kLatPairs;
+    if (threadIdx.x < 64) {
+        // ---- producer wave: pair j on lanes 8j..8j+7 (k_prepare_wide's layout)
+        const int L = (int)threadIdx.x, j = L >> 3, c = L & 1;
+        const bool valid = base + j < n;
+        const size_t pi = valid ? base + j : n - 1;  // idle slots repeat a real pair
+        const int k = pw_slot();
+        const bool st = k == 0;
+        const PairAffine a = pair_to_affine(p, q, pi, pi * kL + c, nullptr, err, valid ? mode : 0);
+        if (st && c == 0) g_lat_skip[j] = a.skip ? 1u : 0u;
+        auto emit = [&](int line, const Ell& e) {
+            const auto x4 = narrow<kLine>(fq2_scale(e.ell_vw, a.py));
+            const auto x2 = narrow<kLine>(fq2_scale(e.ell_vv, a.px));
+            for (uint32_t spins = 0; BN_ANY(valid && line - (int)cons[j] >= kLatRing) && spins < kLatSpinCap; ++spins)
+                __builtin_amdgcn_s_sleep(1);
+            asm volatile("" ::: "memory");
+            if (st) {  // the operand forms c0, c1, -c1 of each coefficient (fq12_wide.h w12_mul_line)
+                uint32_t* ln = g_lat_ring + (j * kLatRing + line % kLatRing) * kLatLineWords;
+                w_put(ln, 0 + c, e.ell_0.c);
+                w_put(ln, 3 + c, x4.c);
+                w_put(ln, 6 + c, x2.c);
+                if (c) {
+                    w_put(ln, 2, fq_neg(e.ell_0.c));
+                    w_put(ln, 5, fq_neg(x4.c));
+                    w_put(ln, 8, fq_neg(x2.c));
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the line is in LDS before it is announced
+            if (st && c == 0) prod[j] = (uint32_t)line + 1;
+        };
+        G2Proj r = {a.qa.x, a.qa.y, widen<kPt>(fq2_one())};
+        const auto qy_neg = fq2_neg(a.qa.y);
+        int line = 0;
+#pragma unroll 1
+        for (int d = 0; d < BN_NAF_DIGITS; ++d) {
+            emit(line++, pw_doubling_step(r, k));
+            if ((kNafNonzero >> d) & 1u) {
+                const bool minus = (kNafMinus >> d) & 1u;
+                const G2Aff<kPt> bq = {a.qa.x, fq2_select(minus, widen<kPt>(qy_neg), a.qa.y)};
+                emit(line++, pw_mixed_addition_step(r, bq, k));
+            }
+        }
+        G2Aff<kPt> q1 = mul_by_q(a.qa);
+        G2Aff<kPt> q2 = mul_by_q(q1);
+        q2.y = narrow<kPt>(fq2_neg(q2.y));
+        emit(line++, pw_mixed_addition_step(r, q1, k));
+        emit(line++, pw_mixed_addition_step(r, q2, k));
+        return;
+    }
+    // ---- consumer groups: pair j on a 16-lane group of waves 1-2
+    const int j = ((int)threadIdx.x - 64) / kWLanes;
+    const size_t pi = base + j;
+    if (pi >= n) return;
+    const WL w = wl();
+    auto ln = [&](int line) { return (uint32_t)((j * kLatRing + line % kLatRing) * kLatLineWords); };
+    auto wait_line = [&](int line) {
+        for (uint32_t spins = 0; prod[j] <= (uint32_t)line && spins < kLatSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+    };
+    auto took = [&](int line) {  // the line's words have been read (the product has returned)
+        asm volatile("" ::: "memory");
+        if (w.l == 0) cons[j] = (uint32_t)line + 1;
+    };
+    int line = 0;
+    wait_line(line);
+    Fq<2> f = w12_from_line(ln(line));  // digit 0 from f = one: one^2 * line = the line
+    took(line++);
+#pragma unroll 1
+    for (int d = 0; d < BN_NAF_DIGITS; ++d) {
+        if (d > 0) {
+            f = w12_mul(f, f);  // the generic square, as the reference's loop
+            wait_line(line);
+            f = w12_mul_line(f, ln(line));
+            took(line++);
+        }
+        if ((kNafNonzero >> d) & 1u) {
+            wait_line(line);
+            f = w12_mul_line(f, ln(line));
+            took(line++);
+        }
+    }
+#pragma unroll 1
+    for (int t = 0; t < 2; ++t) {  // the lines of Q1 and -Q2 (mod.rs:600-604)
+        wait_line(line);
+        f = w12_mul_line(f, ln(line));
+        took(line++);
+    }
+    // a zero point: pairing() is Fq12::one() (mod.rs:896), and FE(one) = one
+    const Fq<2> one = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
+    const Fq<2> x = g_lat_skip[j] ? one : f;
+    if (f_out) {  // the Miller value, for the product of pairing_batch / miller_loop_batch
+        w_st_split(f_out, n, pi, w, x);
+        return;
+    }
+    const bool zero = w12_is_zero(x);
+    if (zero && err && w.l == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+    const Fq<2> res = w12_final_exp(x);
+    uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!zero) fq_store_ref(res, words);
+    if (w.l < 12) st_words(&out[pi].c[w_gt_index(w)], words);
 }
 
 // *status = the bn_status of the device-side outcome bits in *err (bn_*_batch_dev)

@@ -35,6 +35,7 @@ EXPORTS = [
     "bn_g1_from_compressed_many_dev", "bn_g2_from_compressed_many_dev", "bn_gt_pow_many", "bn_gt_pow_many_dev",
     "bn_ctx_create_multi", "bn_ctx_num_devices", "bn_ctx_device", "bn_shard_range", "bn_pairing_many_allgather_dev",
     "bn_pairing_batch_dev", "bn_miller_loop_batch_dev", "bn_set_fe_wide_max", "bn_g2_precompute_many",
+    "bn_set_latency_max",
 ]
 
 # per-element status (bn_elem_status)
@@ -113,6 +114,7 @@ def load():
         "bn_pairing_batch_dev": ([vp, vp, vp, sz, vp, vp, vp], i),
         "bn_miller_loop_batch_dev": ([vp, vp, vp, sz, vp, vp, vp], i),
         "bn_set_fe_wide_max": ([vp, sz], i),
+        "bn_set_latency_max": ([vp, sz], i),
         "bn_g2_precompute_many": ([vp, vp, sz, vp], i),
     }
     for name, (args, res) in sig.items():
@@ -294,6 +296,10 @@ class Context:
     def set_fe_wide_max(self, n):
         """Batches of at most n elements use the 16-lane final exponentiation (latency path)."""
         self._check(self._L.bn_set_fe_wide_max(self._h, n))
+
+    def set_latency_max(self, n):
+        """Latency-path batches of at most n pairs run the one-launch k_pairing_latency."""
+        self._check(self._L.bn_set_latency_max(self._h, n))
 
     def set_phase_timing(self, enable=True):
         self._check(self._L.bn_set_phase_timing(self._h, 1 if enable else 0))

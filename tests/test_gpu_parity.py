@@ -28,6 +28,17 @@ def ctx_tp():
 
 
 @pytest.fixture(scope="module")
+def ctx_seg():
+    """A context whose small pairing_many batches take the segmented latency path
+    (k_prepare_wide + k_miller_seg + k_horner_wide) instead of the one-launch
+    k_pairing_latency."""
+    from substrate_bn import Context
+    c = Context(0)
+    c.set_latency_max(0)
+    return c
+
+
+@pytest.fixture(scope="module")
 def pairs():
     p, q, s, t = O.random_pairs(256, seed=1234, nthreads=NT)
     return p, q
@@ -277,3 +288,27 @@ def test_throughput_path_4096_and_final_exp(ctx_tp):
     keep = np.ones(300, bool)
     keep[7] = False
     assert ok[keep].all() and np.array_equal(fe[keep], want[:300][keep])
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 63, 255])
+def test_latency_paths_ragged(ctx, ctx_seg, pairs, n):
+    """Both latency-path forms -- the one-launch k_pairing_latency (ctx: 8 pairs
+    per block, partial blocks, idle producer slots) and the segmented kernels
+    (ctx_seg) -- against the oracle, zero points in the tail lanes."""
+    p, q = pairs
+    p2, q2 = p[:n].copy(), q[:n].copy()
+    one = O.canon_to_mont_array([1])
+    p2[n - 1] = 0
+    p2[n - 1, 4:8] = one
+    if n > 2:
+        q2[n - 2] = 0
+        q2[n - 2, 8:12] = one
+    want = O.pairing_many(p2, q2, NT)
+    assert np.array_equal(ctx.pairing_many(p2, q2), want)
+    assert np.array_equal(ctx_seg.pairing_many(p2, q2), want)
+
+
+def test_latency_kernel_1024(ctx, pairs):
+    """1024 pairs (the default k_pairing_latency threshold: 128 blocks) bit-exact."""
+    p, q, _, _ = O.random_pairs(1024, seed=1025, nthreads=NT)
+    assert np.array_equal(ctx.pairing_many(p, q), O.pairing_many(p, q, NT))

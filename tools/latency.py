@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--calls", default="pairing_many,pairing_batch,pairing_many_dev")
     ap.add_argument("--fe-wide-max", type=int, default=None,
                     help="batches up to this size take the latency path (bn_set_fe_wide_max)")
+    ap.add_argument("--latency-max", type=int, default=None,
+                    help="latency-path batches up to this size run k_pairing_latency (bn_set_latency_max)")
     args = ap.parse_args()
     import torch
 
@@ -48,6 +50,8 @@ def main():
     ctx = Context(0)
     if args.fe_wide_max is not None:
         ctx.set_fe_wide_max(args.fe_wide_max)
+    if args.latency_max is not None:
+        ctx.set_latency_max(args.latency_max)
     sizes = [int(s) for s in args.sizes.split(",")]
     nmax = max(sizes)
     s, t = synth.dataset_scalars(0, nmax)
@@ -86,7 +90,8 @@ def main():
             fn()
             dt = med(fn, args.reps)
             print(json.dumps({"call": call, "n": n, "ms": dt * 1e3, "per_item_us": dt / n * 1e6,
-                              "cpu_1thread_ms": cpu1 * n * 1e3, "fe_wide_max": args.fe_wide_max}), flush=True)
+                              "cpu_1thread_ms": cpu1 * n * 1e3, "fe_wide_max": args.fe_wide_max,
+                              "latency_max": args.latency_max}), flush=True)
 
 
 if __name__ == "__main__":
