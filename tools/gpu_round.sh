@@ -1,25 +1,35 @@
 #!/bin/bash
-# One GPU-box session: parity tests, bench line, rocprofv3 kernel stats and
-# the three PMC passes (FETCH_SIZE / WRITE_SIZE / SQ), each step time-limited
-# and chained so the first failure ends the call.  Usage: tools/gpu_round.sh TAG
+# One GPU-box measurement session for round TAG: parity tests, the bench line,
+# rocprofv3 kernel stats, the PMC passes (FETCH_SIZE / WRITE_SIZE / two SQ sets),
+# the other BASELINE workloads and the latency sweep.  Each step is time-limited
+# and the first failure ends the call.  Usage: tools/gpu_round.sh TAG
 set -e
 TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-echo "== tests"; timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
-tail -3 $OUT/gpu_tests.log
-echo "== bench"; timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
+Q="--no-cpu-baseline --no-e2e --no-config4-ref"
+echo "== tests"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/gpu_tests.log 2>&1 || { tail -30 $OUT/gpu_tests.log; exit 1; }
+tail -1 $OUT/gpu_tests.log
+echo "== bench"
+timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
-echo "== stats"; timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/prof.err
+echo "== kernel stats"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py $Q > $OUT/bench_prof.json 2> $OUT/prof.err
 echo "== pmc"
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o p -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_fetch.err
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o p -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_write.err
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o p -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_sq.err
-echo "== 8(f) workloads"
-for w in g2validate g2decompress gtpow g1mul; do
-  timeout -k 10 300 python -u bench.py --workload $w --steps 5 --warmup 1 > $OUT/bench_$w.json 2> $OUT/bench_$w.err
-  head -c 400 $OUT/bench_$w.json; echo
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_fetch.err
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_write.err
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_sq.err
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_sq2 -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_sq2.err
+echo "== workloads"
+for w in g1mul product gtpow g2validate g2decompress; do
+  timeout -k 10 300 python -u bench.py --workload $w --steps 10 --warmup 2 > $OUT/bench_$w.json 2> $OUT/bench_$w.err
+  head -c 300 $OUT/bench_$w.json; echo
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_codec -o run -- python3 bench.py --workload g2validate --steps 3 --warmup 1 > /dev/null 2> $OUT/prof_codec.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_product -o run -- python3 bench.py --workload product --steps 10 > /dev/null 2> $OUT/prof_product.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_g1mul -o run -- python3 bench.py --workload g1mul --steps 5 --cpu-sample 64 > /dev/null 2> $OUT/prof_g1mul.err
+echo "== latency"
+timeout -k 10 300 python -u tools/latency.py --calls pairing_many_dev,pairing_many,pairing_batch --sizes 1,2,8,64,256,1024,2048,4096 > $OUT/latency.jsonl 2> $OUT/latency.err
+head -3 $OUT/latency.jsonl
 echo "== done"

@@ -60,7 +60,7 @@ if db is not None:
 
 # ---- PMC passes
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for sub in ("pmc_fetch", "pmc_write", "pmc_sq"):
+for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
     db = one_db(sub + "/*results.db")
     if db is None:
         continue
@@ -109,6 +109,12 @@ for k, v in sorted(agg.items()):
                   # average wave lifetime as a fraction of the kernel (GRBM_GUI_ACTIVE sums the 8 XCDs):
                   # near 1 when the waves of a one-round launch finish together
                   "wave_life_frac": cyc / (m["GRBM_GUI_ACTIVE"] / 8) if m.get("GRBM_GUI_ACTIVE") else None,
+                  # where a wave's cycles go (SQ_* in quad-cycles, per wave): issuing, waiting on
+                  # s_waitcnt (memory / LDS), waiting on a dependency or a busy pipe
+                  "cycles_per_wave": {c: m[c] * 4 / (m.get("SQ_WAVES") or waves)
+                                      for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+                                                "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_MISC")
+                                      if c in m},
                   "note": "FETCH_SIZE corrected by the read factor calibrated on k_fe_out (known bytes), "
                           "WRITE_SIZE as counted (MI355X_MICROARCH §HBM); source %s" % tag}
     lines.append("%-16s %14.3e %14.3e %14.3e %12.3e %10.3f" % (k, fetch, write, valu, cyc, valu / cyc if cyc else 0))
