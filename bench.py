@@ -575,7 +575,11 @@ def run_pairing(args, eng, rank, world, dist):
     if gpu:
         per_launch_ms = {PHASES[k]: phase_ms[k] / max(launches, 1) for k in range(4)}
         fqmul = dict(FQMUL_PER_PAIRING)
-        if per_launch_ms["k_miller"] < 0.01 * per_launch_ms["k_prepare"]:
+        if per_launch_ms["k_fq12_vm"] < 0.01 * per_launch_ms["k_prepare"]:
+            # miller_form 3: the whole pairing is one kernel (k_pairing_full)
+            per_launch_ms = {"k_pairing_full": per_launch_ms["k_prepare"]}
+            fqmul["k_pairing_full"] = sum(FQMUL_PER_PAIRING.values())
+        elif per_launch_ms["k_miller"] < 0.01 * per_launch_ms["k_prepare"]:
             # the default form runs to_affine, the line steps and the Miller loop as one
             # kernel (k_pairing_fused): phase 0 holds both
             per_launch_ms = {"k_pairing_fused": per_launch_ms["k_prepare"], "k_fq12_vm": per_launch_ms["k_fq12_vm"],

@@ -609,6 +609,8 @@ int bn_ctx_create(int device, bn_ctx** out) {
     c->fe_out = (int)build_final_exp(P);
     P.finalize({(uint32_t)c->fe_out});
     c->fe_steps = P.steps();
+    // k_pairing_full returns the last step's result as the Gt: it must be fe_out
+    c->fe_last_out = c->fe_steps > 0 && (int)((P.s[2 * (c->fe_steps - 1)] >> 8) & 0xff) == c->fe_out;
     if (P.next > (uint32_t)kFeSlots) {
         delete c;  // nothing created yet
         return BN_ERR_INVALID_ARGUMENT;
@@ -733,6 +735,17 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             mark(2);
             k_horner_wide<<<grid_for(16 * m), kBlock, 0, s>>>(slot_region(c, kRegionSeg), m, plan, 1, d_out + off,
                                                               c->d_err);
+            mark(3);
+            mark(4);
+            HIPCHK(c, hipGetLastError());
+            if (c->timing) c->ev_marks.push_back(ev);
+            continue;
+        }
+        if (c->miller_form == 3 && c->fe_last_out) {
+            k_pairing_full<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(d_p + off, d_q + off, m, c->d_prog,
+                                                                       c->fe_steps, c->slots, d_out + off, c->d_err);
+            mark(1);
+            mark(2);
             mark(3);
             mark(4);
             HIPCHK(c, hipGetLastError());

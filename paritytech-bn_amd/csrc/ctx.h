@@ -30,6 +30,7 @@ struct bn_ctx {
     std::vector<std::array<hipEvent_t, 5>> ev_marks;
     int fe_steps = 0;
     int fe_out = 0;
+    bool fe_last_out = false;  // the program's last step writes fe_out (k_pairing_full)
     // batches of at most this many elements run the final exponentiation on the
     // wide layout (kernels_wide.hip, 16 lanes per element: latency) instead of
     // the step machine (k_fq12_vm, 2 lanes per element: throughput)
@@ -39,7 +40,7 @@ struct bn_ctx {
     // line steps and Miller loop fused in one kernel (k_pairing_fused, no
     // coefficient traffic); 0 = k_prepare (line coefficients to HBM) + k_miller;
     // 2 = k_prepare + k_miller_seg with one segment
-    int miller_form = 1;
+    int miller_form = 3;  // 3: k_pairing_full; 1: k_pairing_fused + k_fq12_vm + k_fe_out; 0/2: k_prepare + k_miller(_seg) + ...
     // bn_pairing_many_dev batches of at most this many pairs run k_pairing_latency
     size_t latency_max = 0;
     // batches of at most this many pairs take k_prepare_wide (8 lanes per pair)

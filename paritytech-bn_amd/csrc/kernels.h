@@ -537,6 +537,10 @@ __global__ void __launch_bounds__(kPairBlock) k_pairing_fused(const bn_g1* __res
 __global__ void __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ coeffs, const uint32_t* __restrict__ paff,
                          const uint8_t* __restrict__ flags, size_t n, uint32_t* __restrict__ f_out);
 __global__ void __launch_bounds__(kPairBlock) k_fq12_vm(const uint32_t* __restrict__ prog, int nsteps, uint32_t* slots, size_t n);
+__global__ void __launch_bounds__(kPairBlock) k_pairing_full(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
+                                                          size_t n, const uint32_t* __restrict__ prog, int nsteps,
+                                                          uint32_t* __restrict__ slots, bn_gt* __restrict__ out,
+                                                          int* __restrict__ err);
 __global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ slots, size_t n, int out_slot, const uint8_t* __restrict__ flags,
                          bn_gt* __restrict__ out, uint8_t* __restrict__ ok, int* __restrict__ err);
 // kernels_wide.hip (fq12_wide.h): final exponentiation and product reduction on 16-lane groups

@@ -10,14 +10,11 @@
 #include "fq.h"
 #define BN_SPLIT BN_PATH_SPLIT
 #include "kernels.h"
+#include "fe_vm.h"
 
 namespace bn {
 
 constexpr size_t kL = BN_SPLIT ? 2 : 1;  // lanes per element in this translation unit
-
-__device__ __forceinline__ uint32_t* slot_ptr(uint32_t* slots, size_t nl, uint32_t s) {
-    return slots + (size_t)s * kSlotLaneWords * nl;
-}
 
 // Launched with kPairBlock threads per block (kernels.h: two-wave issue balance;
 // the program position is step * 256 + squarings done in the step).
@@ -27,59 +24,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_fq12_vm(const uint3
     const Balance bal = balance_init();
     const size_t i = lane_id();
     if (i >= kL * n) return;
-    Fq12<kF> acc = widen<kF>(fq12_one());  // the previous step's result, kept in registers
-#pragma unroll 1
-    for (int pc = 0; pc < nsteps; ++pc) {
-        const uint32_t ins = prog[2 * pc];  // uniform: scalar loads
-        const uint32_t aux = prog[2 * pc + 1];
-        const uint32_t op = ins & 0xff, k = aux & 0xff, flags = aux >> 8;
-        // The slot stride passes through an empty asm once per step, so the
-        // word offsets of a lane-strided Fq12 (w * nl, uniform) are rebuilt where
-        // they are used instead of being hoisted out of the step loop, where they
-        // would occupy ~216 SGPRs and spill through VGPR lanes.
-        size_t nn = kL * n;
-        asm volatile("" : "+s"(nn));
-        uint32_t* d = slot_ptr(slots, nn, (ins >> 8) & 0xff);
-        const uint32_t* a = slot_ptr(slots, nn, (ins >> 16) & 0xff);
-        const uint32_t* b = slot_ptr(slots, nn, ins >> 24);
-        balance_step(bal, (uint32_t)pc << 8);
-        Fq12<kF> x;
-        if (flags & kFlagAccA) x = acc; else x = ld_fq12_buf<kF>(a, nn, i);
-        Fq12<kF> r;
-        switch (op) {
-            case OP_MOV: r = x; break;
-            case OP_MUL: {
-#pragma unroll 1
-                for (uint32_t j = 0; j < k; ++j) {
-                    balance_step(bal, ((uint32_t)pc << 8) | j);
-                    x = cyc_sqr(x);
-                }
-                balance_step(bal, ((uint32_t)pc << 8) | 255u);
-                Fq12<kF> y = ld_fq12_buf<kF>(b, nn, i);
-                if (flags & kFlagConjB) y = fq12_conj(y);
-                r = mul12(x, y);
-                if (flags & kFlagConjOut) r = fq12_conj(r);
-                break;
-            }
-            case OP_SQR: r = narrow12<kF>(fq12_sqr(x)); break;
-            case OP_CYC: {
-#pragma unroll 1
-                for (uint32_t j = 0; j < k; ++j) {
-                    balance_step(bal, ((uint32_t)pc << 8) | j);
-                    x = cyc_sqr(x);
-                }
-                r = x;
-                break;
-            }
-            case OP_CONJ: r = fq12_conj(x); break;
-            case OP_FROB1: r = narrow12<kF>(fq12_frobenius_map<1>(x)); break;
-            case OP_FROB2: r = narrow12<kF>(fq12_frobenius_map<2>(x)); break;
-            case OP_FROB3: r = narrow12<kF>(fq12_frobenius_map<3>(x)); break;
-            default: r = narrow12<kF>(fq12_inv(x)); break;  // OP_INV
-        }
-        acc = r;
-        if (!(flags & kFlagNoStore)) st_fq12_buf(d, nn, i, r);
-    }
+    (void)fq12_vm_run(prog, nsteps, slots, kL * n, i, bal, 0, true);
 }
 
 // out[e] = slot `out_slot`; slot 0 holds the Miller value: f == 0 means the

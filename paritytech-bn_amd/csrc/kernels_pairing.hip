@@ -11,6 +11,7 @@
 #define BN_SPLIT BN_PATH_SPLIT
 #include "kernels.h"
 #include "lines_wide.h"
+#include "fe_vm.h"
 
 namespace bn {
 
@@ -118,6 +119,40 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_pairing_fused(const
     Fq12<kF> f = miller_fused(a.qa, a.px, a.py, [&](int d) { balance_step(bal, (uint32_t)d); });
     if (flags[l]) f = widen<kF>(fq12_one());
     st_fq12(f_out, nl, l, f);
+}
+
+// A/B form (miller_form 3): k_pairing_fused, k_fq12_vm and
+// k_fe_out as one kernel.  The Miller value is stored to slot 0 (the step
+// program reads it more than once) and the program runs right behind it on the
+// same lanes; its last step's result (slot `out_slot`, checked by the host) is
+// written straight to out[] as k_fe_out would.  Removes the two kernel tails
+// between the phases (a wave waits for the slowest wave of the grid at each
+// boundary).  Balance positions of the program are offset past the loop's.
+__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_pairing_full(const bn_g1* __restrict__ p,
+                                                                         const bn_g2* __restrict__ q, size_t n,
+                                                                         const uint32_t* __restrict__ prog, int nsteps,
+                                                                         uint32_t* __restrict__ slots,
+                                                                         bn_gt* __restrict__ out, int* __restrict__ err) {
+    fold_table_init();
+    const Balance bal = balance_init();
+    const size_t l = lane_id(), i = l / kL, nl = kL * n;
+    if (i >= n) return;
+    const PairAffine a = pair_to_affine(p, q, i, l, nullptr, err, 0);
+    Fq12<kF> f = miller_fused(a.qa, a.px, a.py, [&](int d) { balance_step(bal, (uint32_t)d); });
+    if (a.skip) f = widen<kF>(fq12_one());
+    // f == 0: the reference's final_exponentiation returns None and pairing()
+    // panics (fq12.rs:63-72) -> zero Gt and the error bit, as k_fe_out
+    const bool zero = !a.skip && fq12_is_zero(f);
+    st_fq12(slots, nl, l, f);
+    const Fq12<kF> r = fq12_vm_run(prog, nsteps, slots, nl, l, bal, 1u << 20, false);
+    if (zero) {
+        if ((l % kL) == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        st_gt_zero(out[i]);
+    } else if (a.skip) {
+        st_gt(out[i], fq12_one());
+    } else {
+        st_gt(out[i], r);
+    }
 }
 
 __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* __restrict__ coeffs,

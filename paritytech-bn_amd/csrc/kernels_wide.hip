@@ -138,6 +138,22 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
 __shared__ uint32_t g_lat_prod[kLatPairs], g_lat_cons[kLatPairs], g_lat_skip[kLatPairs];
 constexpr uint32_t kLatSpinCap = 1u << 26;  // ~4 s of s_sleep 1: never reached while both sides run
 
+// Diagnostic build (-DBN_LAT_STAMPS=1, tools/lat_stamps.py): block 0 records
+// s_memrealtime (100 MHz) at the phase boundaries of its first pair into a
+// buffer read by bn_dbg_lat_stamps(); the product build has none of it.
+#ifndef BN_LAT_STAMPS
+#define BN_LAT_STAMPS 0
+#endif
+#if BN_LAT_STAMPS
+__device__ uint64_t g_lat_stamps[8];
+#define LAT_STAMP(cond, k)                                                            \
+    do {                                                                              \
+        if (blockIdx.x == 0 && (cond)) g_lat_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define LAT_STAMP(cond, k) ((void)0)
+#endif
+
 // f_out != null (pairing_batch / miller_loop_batch): the Miller values go to
 // f_out (split layout, lane-strided, stride n; a zero-point pair's is one) for the
 // product reduction, and no final exponentiation runs here; mode 1
@@ -156,6 +172,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
     volatile uint32_t* prod = g_lat_prod;
     volatile uint32_t* cons = g_lat_cons;
     const size_t base = (size_t)blockIdx.x * kLatPairs;
+    LAT_STAMP(threadIdx.x == 0, 0);  // start
     if (threadIdx.x < 64) {
         // ---- producer wave: pair j on lanes 8j..8j+7 (k_prepare_wide's layout)
         const int L = (int)threadIdx.x, j = L >> 3, c = L & 1;
@@ -164,6 +181,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
         const int k = pw_slot();
         const bool st = k == 0;
         const PairAffine a = pair_to_affine(p, q, pi, pi * kL + c, nullptr, err, valid ? mode : 0);
+        LAT_STAMP(threadIdx.x == 0, 1);  // producer: to_affine done
         if (st && c == 0) g_lat_skip[j] = a.skip ? 1u : 0u;
         auto emit = [&](int line, const Ell& e) {
             const auto x4 = narrow<kLine>(fq2_scale(e.ell_vw, a.py));
@@ -202,6 +220,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
         q2.y = narrow<kPt>(fq2_neg(q2.y));
         emit(line++, pw_mixed_addition_step(r, q1, k));
         emit(line++, pw_mixed_addition_step(r, q2, k));
+        LAT_STAMP(threadIdx.x == 0, 2);  // producer: last line out
         return;
     }
     // ---- consumer groups: pair j on a 16-lane group of waves 1-2
@@ -220,6 +239,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
     };
     int line = 0;
     wait_line(line);
+    LAT_STAMP(threadIdx.x == 64, 3);  // consumer: first line in
     Fq<2> f = w12_from_line(ln(line));  // digit 0 from f = one: one^2 * line = the line
     took(line++);
 #pragma unroll 1
@@ -242,6 +262,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
         f = w12_mul_line(f, ln(line));
         took(line++);
     }
+    LAT_STAMP(threadIdx.x == 64, 4);  // consumer: Miller loop done
     // a zero point: pairing() is Fq12::one() (mod.rs:896), and FE(one) = one
     const Fq<2> one = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
     const Fq<2> x = g_lat_skip[j] ? one : f;
@@ -252,6 +273,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
     const bool zero = w12_is_zero(x);
     if (zero && err && w.l == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
     const Fq<2> res = w12_final_exp(x);
+    LAT_STAMP(threadIdx.x == 64, 5);  // consumer: final exponentiation done
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!zero) fq_store_ref(res, words);
     if (w.l < 12) st_words(&out[pi].c[w_gt_index(w)], words);
@@ -266,3 +288,9 @@ __global__ void __launch_bounds__(kBlock) k_err_status(const int* __restrict__ e
 }
 
 }  // namespace bn
+
+#if BN_LAT_STAMPS
+extern "C" int bn_dbg_lat_stamps(uint64_t out[8]) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(bn::g_lat_stamps), 8 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif

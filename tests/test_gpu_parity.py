@@ -19,8 +19,8 @@ def ctx():
 @pytest.fixture(scope="module")
 def ctx_tp():
     """A context whose every pairing_many batch takes the THROUGHPUT path
-    (k_pairing_fused + k_fq12_vm + k_fe_out, the kernels bench.py's `value`
-    measures): the latency-path threshold is 0."""
+    (k_pairing_full, the kernel bench.py's `value` measures): the latency-path
+    threshold is 0."""
     from substrate_bn import Context
     c = Context(0)
     c.set_fe_wide_max(0)
@@ -272,6 +272,26 @@ def test_throughput_path_ragged(ctx_tp, pairs, n):
         q2[n - 2] = 0
         q2[n - 2, 8:12] = one        # G2::zero() in the lane before it
     assert np.array_equal(ctx_tp.pairing_many(p2, q2), O.pairing_many(p2, q2, NT))
+
+
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_throughput_path_other_forms(pairs, form, monkeypatch):
+    """The A/B forms of the throughput path (BN254MI_MILLER_FORM):
+    0 = k_prepare + k_miller, 1 = k_pairing_fused, 2 = k_prepare + k_miller_seg (one
+    segment), each followed by k_fq12_vm + k_fe_out -- the same Gt as k_pairing_full,
+    zero points included."""
+    from substrate_bn import Context
+    monkeypatch.setenv("BN254MI_MILLER_FORM", str(form))
+    c = Context(0)
+    c.set_fe_wide_max(0)
+    p, q = pairs
+    p2, q2 = np.concatenate([p, p[:44]]), np.concatenate([q, q[:44]])  # 300 pairs
+    one = O.canon_to_mont_array([1])
+    p2[7] = 0
+    p2[7, 4:8] = one
+    q2[299] = 0
+    q2[299, 8:12] = one
+    assert np.array_equal(c.pairing_many(p2, q2), O.pairing_many(p2, q2, NT))
 
 
 def test_throughput_path_4096_and_final_exp(ctx_tp):
