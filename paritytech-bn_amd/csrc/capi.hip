@@ -349,7 +349,7 @@ int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, size_t n, size
 // (whose program reads and writes the slots from slot 0: f must be slot 0)
 int run_fe(bn_ctx* c, const uint32_t* f, size_t n, const uint8_t* flags, bn_gt* out, uint8_t* ok, hipStream_t s) {
     if (n <= c->fe_wide_max) {
-        k_fe_wide<<<grid_for(16 * n), kBlock, 0, s>>>(f, n, n, out, ok, c->d_err);
+        k_fe_wide<<<wide_blocks(n), kBlock, 0, s>>>(f, n, n, out, ok, c->d_err, wide_duo(n) ? 1 : 0);
         HIPCHK(c, hipGetLastError());
         return BN_OK;
     }
@@ -439,7 +439,7 @@ int finish_product(bn_ctx* c, const SegPlan& plan, size_t nchunks, int do_fe, bn
     if (nchunks > 1)
         RET_IF(product_wide(c, slot_region(c, kRegionParts), plan.S * nchunks, nchunks, nchunks, plan.S,
                             slot_region(c, kRegionResult), plan.S, 0, 1, s));
-    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, plan, do_fe, d_out, c->d_err);
+    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, plan, do_fe, d_out, c->d_err, wide_duo(1) ? 1 : 0);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
@@ -455,7 +455,7 @@ int latency_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int
     HIPCHK(c, hipGetLastError());
     RET_IF(product_wide(c, slot_region(c, kRegionSeg), n, n, n, 1, slot_region(c, kRegionResult), 1, 0, 1, s));
     const SegPlan whole = cut_plan(1, 1);  // one segment: x = the product, then the FE when do_fe
-    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, whole, do_fe, d_out, c->d_err);
+    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, whole, do_fe, d_out, c->d_err, wide_duo(1) ? 1 : 0);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
@@ -733,8 +733,8 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             k_miller_seg<<<grid_pair(kPathLanes * plan.S * m), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
                                                                                slot_region(c, kRegionSeg));
             mark(2);
-            k_horner_wide<<<grid_for(16 * m), kBlock, 0, s>>>(slot_region(c, kRegionSeg), m, plan, 1, d_out + off,
-                                                              c->d_err);
+            k_horner_wide<<<wide_blocks(m), kBlock, 0, s>>>(slot_region(c, kRegionSeg), m, plan, 1, d_out + off,
+                                                              c->d_err, wide_duo(m) ? 1 : 0);
             mark(3);
             mark(4);
             HIPCHK(c, hipGetLastError());

@@ -31,10 +31,10 @@ static_assert(BN_SPLIT, "fq12_wide.h builds on the two-lane Fq2 of fq2_split.h")
 constexpr int kWLanes = 16;                         // lanes per element (12 hold coordinates)
 constexpr int kWSlot = 12;                          // words per LDS slot: one Fq, 48 B aligned
 constexpr int kWArr = kWLanes * kWSlot;             // words of one operand array of a group
-constexpr int kWArrs = 4;                           // operand arrays per group
-constexpr int kWGroupWords = kWArrs * kWArr;        // 3 KB per group
+constexpr int kWArrs = 5;                           // operand arrays per group
+constexpr int kWGroupWords = kWArrs * kWArr;        // 3.75 KB per group
 constexpr int kWGroups = kBlock / kWLanes;          // 16 groups per 256-thread block
-__shared__ uint32_t g_wide[kWGroups * kWGroupWords];  // 48 KB
+__shared__ uint32_t g_wide[kWGroups * kWGroupWords];  // 60 KB
 
 // this lane's place in its group
 struct WL {
@@ -116,6 +116,66 @@ __device__ __noinline__ Fq<2> w12_mul(Fq<2> a, Fq<2> b) {
         if (i == 2) acc_carry_par(t);  // six normalized products per batch keep columns < 2^64
     }
     // value <= 12 * (2p)^2: the result is below (48 p / 2^261 + 1) p < 2p
+    return acc_redc<2>(t);
+}
+
+// a^2 (fq12.rs:319-327 with b = a), the schoolbook sum folded by symmetry: out_e
+// = sum over i + j = e (mod 6) of a'_i a_j pairs each unordered {i, j}, i != j,
+// twice, so out_e = 2 * (sum over the cross pairs of xi^w a_i a_j + sum over
+// the squares of xi^w a_i (a_i / 2)), w = [i + j >= 6] (w^6 = xi).  Every lane
+// has at most four such terms (two cross + two squares for even e, three cross
+// for odd e): eight digit products instead of twelve, one doubling of the
+// columns, one reduction.  The same residues as w12_mul(a, a).
+// Per lane e, term t: operand source of x (0 = a, 1 = xi a, 2 = a/2, 3 = xi a / 2)
+// and the indices i (of x) and j (of y = a); source 3 with i = 6 reads the zero
+// slots 12, 13 of the xi a / 2 array (an absent fourth term).
+constexpr uint64_t w_sqr_code(int src, int i, int j) { return (uint64_t)(src | (i << 2) | (j << 5)); }
+constexpr uint64_t w_sqr_term(uint64_t e0, uint64_t e1, uint64_t e2, uint64_t e3, uint64_t e4, uint64_t e5) {
+    return e0 | (e1 << 8) | (e2 << 16) | (e3 << 24) | (e4 << 32) | (e5 << 40);
+}
+constexpr uint64_t kWSqrTerm[4] = {
+    w_sqr_term(w_sqr_code(1, 1, 5), w_sqr_code(0, 0, 1), w_sqr_code(0, 0, 2), w_sqr_code(0, 0, 3), w_sqr_code(0, 0, 4), w_sqr_code(0, 0, 5)),
+    w_sqr_term(w_sqr_code(1, 2, 4), w_sqr_code(1, 2, 5), w_sqr_code(1, 3, 5), w_sqr_code(0, 1, 2), w_sqr_code(0, 1, 3), w_sqr_code(0, 1, 4)),
+    w_sqr_term(w_sqr_code(2, 0, 0), w_sqr_code(1, 3, 4), w_sqr_code(2, 1, 1), w_sqr_code(1, 4, 5), w_sqr_code(2, 2, 2), w_sqr_code(0, 2, 3)),
+    w_sqr_term(w_sqr_code(3, 3, 3), w_sqr_code(3, 6, 0), w_sqr_code(3, 4, 4), w_sqr_code(3, 6, 0), w_sqr_code(3, 5, 5), w_sqr_code(3, 6, 0)),
+};
+#ifndef BN_WIDE_SQR
+#define BN_WIDE_SQR 1  // 0: squares by w12_mul(a, a) (A/B)
+#endif
+__device__ __noinline__ Fq<2> w12_sqr(Fq<2> a) {
+    const WL w = wl();
+    uint32_t* A_ = w.gb;
+    uint32_t* X_ = w.gb + kWArr;
+    uint32_t* N_ = w.gb + 2 * kWArr;
+    uint32_t* H_ = w.gb + 3 * kWArr;
+    uint32_t* XH_ = w.gb + 4 * kWArr;
+    const Fq<2> xa = w_xi(a);
+    w_put(A_, w.l, a);
+    w_put(X_, w.l, xa);
+    w_put(N_, w.l, fq_neg(a));
+    w_put(H_, w.l, fq_half(a));
+    w_put(XH_, w.l, w.l < 12 ? fq_half(xa) : widen<2>(fq_zero()));  // slots 12..15: the zero operand
+    w_sync();
+    Acc t = {};
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+        const uint64_t tq = q == 0 ? kWSqrTerm[0] : q == 1 ? kWSqrTerm[1] : q == 2 ? kWSqrTerm[2] : kWSqrTerm[3];
+        const uint32_t code = (uint32_t)(tq >> (8 * w.e)) & 0xffu;
+        const uint32_t src = code & 3u, i = (code >> 2) & 7u, j = code >> 5;
+        const uint32_t* xs = src == 0 ? A_ : src == 1 ? X_ : src == 2 ? H_ : XH_;
+        const Fq<2> x0 = w_get<2>(xs, (int)(2 * i)), x1 = w_get<2>(xs, (int)(2 * i + 1));
+        // c0: x0*y0 + x1*(-y1), c1: x0*y1 + x1*y0
+        const Fq<2> yo = w_get<2>(A_, (int)(2 * j) + w.c);
+        const Fq<2> yx = w_get<2>(w.c ? A_ : N_, (int)(2 * j) + 1 - w.c);
+        acc_mad(t, x0, yo);
+        acc_mad(t, x1, yx);
+        if (q == 2) acc_carry_par(t);  // six normalized products per batch keep columns < 2^64
+    }
+    // columns < 2^36 + 18 * 2^58, doubled < 2^37 + 36 * 2^58: with the reduction's
+    // nine m*p products and its carries they stay below 2^64
+#pragma unroll
+    for (int k = 0; k < 17; ++k) t.c[k] <<= 1;
+    // value <= 2 * 8 * (2p)^2: the result is below (64 p / 2^261 + 1) p < 2p
     return acc_redc<2>(t);
 }
 
@@ -346,6 +406,148 @@ __device__ __noinline__ Fq<2> w12_final_exp(Fq<2> f) {
     const Fq<2> t = w12_mul(w12_conj(s), l);
     const Fq<2> u = w12_frob<3>(t);
     return w12_mul(u, r);
+}
+
+
+// ---------------------------------------------------------------- two-group final exponentiation
+// The same final exponentiation on TWO 16-lane groups of one element, in
+// different waves: a squarer S runs the chain of dependent squarings and a
+// multiplier M folds the products in beside it, so most products leave the
+// critical path (a lone wave issues one v_mad_u64_u32 per ~9.5 cycles whatever
+// the dependences, profiles/r3j_mad_issue.txt: the two groups' streams run in
+// parallel on their SIMDs).  exp_by_neg_z right to left over the NAF of u:
+// x^u = prod over the nonzero digits d_k of (x^(2^k))^(d_k), x^-1 = conj(x) in
+// the cyclotomic subgroup.  S squares x 62 times and hands over x^(2^k) at each
+// of the 24 nonzero digits; M multiplies them into its accumulator (at least two
+// squarings apart, so M keeps up) and returns conj(acc).  The values are the
+// reference's (fq12.rs:75-110): the same group elements, another addition chain.
+// Channel (LDS, per element): a ring of kDuoRing S -> M items and two M -> S
+// result slots; counters cnt[0] = items published by S, cnt[1] = items taken by
+// M, cnt[2] = results published by M.  A writer waits for its LDS writes
+// (lgkmcnt(0)) before bumping a counter; a reader spins on the counter
+// (s_sleep) and then reads -- a wave runs its LDS operations in order.
+struct ZNaf {
+    uint64_t nz = 0, minus = 0;  // digit positions, negative digits
+    int top = 0, n = 0;
+};
+constexpr ZNaf z_naf() {
+    ZNaf r;
+    uint64_t u = 4965661367192848881ull;
+    for (int pos = 0; u; ++pos, u >>= 1) {
+        if (!(u & 1)) continue;
+        const bool neg = (u & 3) == 3;  // digit -1 when u = 3 mod 4
+        r.nz |= 1ull << pos;
+        if (neg) r.minus |= 1ull << pos;
+        r.top = pos;
+        ++r.n;
+        u = neg ? u + 1 : u - 1;
+    }
+    return r;
+}
+constexpr ZNaf kZNaf = z_naf();
+static_assert(kZNaf.top == 62 && kZNaf.n == 24, "NAF of u");
+
+constexpr int kDuoRing = 4;                       // S -> M items in flight
+constexpr int kDuoWords = (kDuoRing + 2) * kWArr;  // channel words per element
+constexpr uint32_t kDuoSpinCap = 1u << 26;        // ~4 s of s_sleep 1: never reached while both run
+
+__device__ __forceinline__ void duo_wait(const volatile uint32_t* c, uint32_t v) {
+    for (uint32_t spins = 0; *c < v && spins < kDuoSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void duo_signal(volatile uint32_t* c, uint32_t v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the data (or the reads) are done first
+    if ((threadIdx.x & (kWLanes - 1)) == 0) *c = v;
+}
+struct WDuo {
+    uint32_t* ch;           // kDuoWords words of LDS
+    volatile uint32_t* cnt;  // three counters, zero at the start
+    uint32_t items, results;
+    __device__ void put(const Fq<2>& x) {  // S
+        if (items >= (uint32_t)kDuoRing) duo_wait(cnt + 1, items + 1 - kDuoRing);
+        w_put(ch + (items % kDuoRing) * kWArr, (int)(threadIdx.x & (kWLanes - 1)), x);
+        duo_signal(cnt, ++items);
+    }
+    __device__ Fq<2> take() {  // M
+        duo_wait(cnt, items + 1);
+        const Fq<2> x = w_get<2>(ch + (items % kDuoRing) * kWArr, (int)(threadIdx.x & (kWLanes - 1)));
+        duo_signal(cnt + 1, ++items);
+        return x;
+    }
+    __device__ void put_result(const Fq<2>& x) {  // M
+        w_put(ch + (kDuoRing + results % 2) * kWArr, (int)(threadIdx.x & (kWLanes - 1)), x);
+        duo_signal(cnt + 2, ++results);
+    }
+    __device__ Fq<2> get_result() {  // S
+        duo_wait(cnt + 2, results + 1);
+        const Fq<2> x = w_get<2>(ch + (kDuoRing + results % 2) * kWArr, (int)(threadIdx.x & (kWLanes - 1)));
+        ++results;
+        return x;
+    }
+};
+// S's side of exp_by_neg_z
+__device__ __noinline__ Fq<2> w12_exp_sq(Fq<2> x, WDuo& d) {
+#pragma unroll 1
+    for (int k = 0;; ++k) {
+        if ((kZNaf.nz >> k) & 1u) d.put(x);
+        if (k == kZNaf.top) break;
+        x = w12_cyc(x);
+    }
+    return d.get_result();
+}
+// M's side: the product of the handed-over powers; returns the first (x itself)
+__device__ __noinline__ Fq<2> w12_exp_mul(WDuo& d) {
+    const Fq<2> x = d.take();  // digit 0 is nonzero (u is odd)
+    Fq<2> acc = (kZNaf.minus & 1u) ? w12_conj(x) : x;
+#pragma unroll 1
+    for (int k = 1; k <= kZNaf.top; ++k) {
+        if (!((kZNaf.nz >> k) & 1u)) continue;
+        const Fq<2> y = d.take();
+        acc = w12_mul(acc, ((kZNaf.minus >> k) & 1u) ? w12_conj(y) : y);
+    }
+    d.put_result(w12_conj(acc));
+    return x;
+}
+// final_exponentiation (fq12.rs:107-110) of f on S; returns the result on S.
+// The hand-overs: [24 powers of s], b, [24 powers of d], [24 powers of f1], k.
+// M returns a, e, g and then o = frob(k*b), u = frob^3(conj(s)*k*b) while S
+// forms m, n and q (the reference's names, fq12.rs:75-105).
+__device__ __noinline__ Fq<2> w12_final_exp_s(Fq<2> f, WDuo& d) {
+    const Fq<2> b0 = w12_inv(f);
+    const Fq<2> c0 = w12_mul(w12_conj(f), b0);
+    const Fq<2> d0 = w12_frob<2>(c0);
+    const Fq<2> s = w12_mul(d0, c0);
+    const Fq<2> a = w12_exp_sq(s, d);
+    const Fq<2> b = w12_cyc(a);
+    d.put(b);
+    const Fq<2> c = w12_cyc(b);
+    const Fq<2> dd = w12_mul(c, b);
+    const Fq<2> e = w12_exp_sq(dd, d);
+    const Fq<2> f1 = w12_cyc(e);
+    const Fq<2> g = w12_exp_sq(f1, d);
+    const Fq<2> j = w12_mul(w12_conj(g), e);
+    const Fq<2> k = w12_mul(j, w12_conj(dd));
+    d.put(k);
+    const Fq<2> m = w12_mul(k, e);
+    const Fq<2> n = w12_mul(s, m);
+    const Fq<2> q = w12_frob<2>(k);
+    const Fq<2> o = d.get_result();
+    const Fq<2> pp = w12_mul(o, n);
+    const Fq<2> r = w12_mul(q, pp);
+    const Fq<2> u = d.get_result();
+    return w12_mul(u, r);
+}
+// M's part of the same final exponentiation
+__device__ __noinline__ void w12_final_exp_m(WDuo& d) {
+    const Fq<2> s = w12_exp_mul(d);  // a
+    const Fq<2> b = d.take();
+    (void)w12_exp_mul(d);            // e
+    (void)w12_exp_mul(d);            // g
+    const Fq<2> k = d.take();
+    const Fq<2> l = w12_mul(k, b);
+    d.put_result(w12_frob<1>(l));    // o
+    const Fq<2> t = w12_mul(w12_conj(s), l);
+    d.put_result(w12_frob<3>(t));    // u
 }
 
 }  // namespace bn

@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(kPairBlock) k_miller_seg(const uint32_t* __res
 // split layout, stride S * n): x = g0; x = x^(2^len_s) * g_s; then the final
 // exponentiation when do_fe
 __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, size_t n, SegPlan plan,
-                                                        int do_fe, bn_gt* __restrict__ out, int* __restrict__ err);
+                                                        int do_fe, bn_gt* __restrict__ out, int* __restrict__ err, int duo);
 __global__ void __launch_bounds__(kPairBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
                           uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
                           int* __restrict__ err, int mode);
@@ -546,14 +546,24 @@ __global__ void __launch_bounds__(kBlock) k_fe_out(const uint32_t* __restrict__ 
 // kernels_wide.hip (fq12_wide.h): final exponentiation and product reduction on 16-lane groups
 __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__ f, size_t stride, size_t n,
                                                     bn_gt* __restrict__ out, uint8_t* __restrict__ ok,
-                                                    int* __restrict__ err);
+                                                    int* __restrict__ err, int duo);
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
                                                              size_t n, size_t in_set, uint32_t* __restrict__ out,
                                                              size_t out_stride, size_t out_base, size_t out_set);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
 // (a producer wave for the lines, consumer groups for the wide Miller loop + FE)
 constexpr int kLatPairs = 8;
-constexpr int kLatThreads = 64 + kLatPairs * 16;  // 192: one producer wave, two consumer waves
+#ifndef BN_FE_DUO
+#define BN_FE_DUO 1  // the latency kernels' final exponentiation on two groups (fq12_wide.h)
+#endif
+// one producer wave, two consumer waves (+ with BN_FE_DUO a wave of multiplier groups)
+constexpr int kLatThreads = 64 + kLatPairs * 16 + (BN_FE_DUO ? 64 : 0);
+// k_fe_wide / k_horner_wide: the two-group final exponentiation (8 elements per
+// block) while the blocks fit one round on the 256 CUs (the channel makes it one
+// block per CU); above, one group per element (16 per block)
+constexpr size_t kWideDuoMax = 2048;
+inline bool wide_duo(size_t n) { return BN_FE_DUO && n <= kWideDuoMax; }
+inline unsigned wide_blocks(size_t n) { return (unsigned)(wide_duo(n) ? (n + 7) / 8 : (n + 15) / 16); }
 __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __restrict__ p,
                                                                  const bn_g2* __restrict__ q, size_t n,
                                                                  bn_gt* __restrict__ out, uint32_t* __restrict__ f_out,

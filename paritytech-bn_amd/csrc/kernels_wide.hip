@@ -7,6 +7,11 @@
 #ifndef BN_FOLD_LDS
 #define BN_FOLD_LDS 1
 #endif
+// 1: idle groups of a block (past n) run on a copy of the last element instead
+// of returning (A/B: the cost of a wave with a single active group)
+#ifndef BN_WIDE_PAD
+#define BN_WIDE_PAD 1
+#endif
 #include "fq.h"
 #define BN_SPLIT 1
 #include "fq12_wide.h"
@@ -25,25 +30,93 @@ __device__ __forceinline__ void w_st_split(uint32_t* f, size_t stride, size_t e,
     if (w.l < 12) st_fq(f, 2 * stride, 2 * e + w.c, w_tower_index(w), x);
 }
 
+// Element and role of this group in the final-exponentiation kernels: with
+// BN_FE_DUO a block holds kWGroups / 2 elements, each with its squarer group in
+// waves 0-1 and its multiplier group in waves 2-3 (fq12_wide.h), and channel
+// `slot` of the block; else one element per group, every group a squarer.
+struct WRole {
+    size_t e;
+    bool sq, duo;
+    int slot;
+};
+constexpr int kDuoPerBlock = kWGroups / 2;
+__device__ __forceinline__ WRole w_role(bool duo) {
+#if BN_FE_DUO
+    if (duo) {
+        const int g = (int)threadIdx.x / kWLanes;
+        return {(size_t)blockIdx.x * kDuoPerBlock + (size_t)(g % kDuoPerBlock), g < kDuoPerBlock, true, g % kDuoPerBlock};
+    }
+#endif
+    (void)duo;
+    return {w_elem(), true, false, 0};
+}
+#if BN_FE_DUO
+__shared__ uint32_t g_wduo_ch[kDuoPerBlock * kDuoWords];  // 36 KB
+__shared__ uint32_t g_wduo_cnt[kDuoPerBlock * 4];
+#endif
+// zero the block's channel counters (every thread of the block calls it)
+__device__ __forceinline__ void w_duo_init() {
+#if BN_FE_DUO
+    if (threadIdx.x < kDuoPerBlock * 4) g_wduo_cnt[threadIdx.x] = 0;
+    __syncthreads();
+#endif
+}
+// the final exponentiation on S (with its M running w12_final_exp_m), or on
+// the group alone
+__device__ __forceinline__ Fq<2> w_final_exp(const WRole& r, const Fq<2>& x) {
+#if BN_FE_DUO
+    if (r.duo) {
+        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0};
+        return w12_final_exp_s(x, d);
+    }
+#endif
+    (void)r;
+    return w12_final_exp(x);
+}
+// M's part; true if this group is M (and has done it)
+__device__ __forceinline__ bool w_final_exp_m(const WRole& r, bool run) {
+#if BN_FE_DUO
+    if (r.sq) return false;
+    if (run) {
+        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0};
+        w12_final_exp_m(d);
+    }
+    return true;
+#else
+    (void)r;
+    (void)run;
+    return false;
+#endif
+}
+
 // out[e] = final_exponentiation(f[e]) for e < n, f lane-strided (split layout,
 // stride `stride`).  f == 0: zero image, ok = 0, error bit (fq12.rs:63-72;
 // pairing() panics, mod.rs:900).  A skipped pair's Miller value is already
 // Fq12::one() (k_miller), and FE(one) = one.
 __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__ f, size_t stride, size_t n,
                                                     bn_gt* __restrict__ out, uint8_t* __restrict__ ok,
-                                                    int* __restrict__ err) {
+                                                    int* __restrict__ err, int duo) {
     fold_table_init();
-    const size_t e = w_elem();
+    w_duo_init();
+    const WRole role = w_role(duo != 0);
+#if BN_WIDE_PAD
+    const bool live = role.e < n;
+    const size_t e = live ? role.e : n - 1;  // idle groups of the block repeat the last element
+#else
+    const bool live = true;
+    const size_t e = role.e;
     if (e >= n) return;
+#endif
+    if (w_final_exp_m(role, true)) return;
     const WL w = wl();
     const Fq<2> x = w_ld_split(f, stride, e, w);
     const bool zero = w12_is_zero(x);
-    if (ok && w.l == 0) ok[e] = zero ? 0 : 1;
-    if (zero && err && w.l == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
-    const Fq<2> r = w12_final_exp(x);
+    if (ok && w.l == 0 && live) ok[e] = zero ? 0 : 1;
+    if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+    const Fq<2> r = w_final_exp(role, x);
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!zero) fq_store_ref(r, words);
-    if (w.l < 12) st_words(&out[e].c[w_gt_index(w)], words);
+    if (w.l < 12 && live) st_words(&out[e].c[w_gt_index(w)], words);
 }
 
 // Product reduction of several independent sets (blockIdx.y = set y, the
@@ -90,35 +163,45 @@ __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __r
 // (pairing / pairing_batch; zero -> zero image + error bit) or the Miller value
 // itself (miller_loop_batch) -> out[e].
 __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, size_t n, SegPlan plan,
-                                                        int do_fe, bn_gt* __restrict__ out, int* __restrict__ err) {
+                                                        int do_fe, bn_gt* __restrict__ out, int* __restrict__ err,
+                                                        int duo) {
     fold_table_init();
-    const size_t e = w_elem();
+    w_duo_init();
+    const WRole role = w_role(duo != 0);
+#if BN_WIDE_PAD
+    const bool live = role.e < n;
+    const size_t e = live ? role.e : n - 1;  // idle groups of the block repeat the last element
+#else
+    const bool live = true;
+    const size_t e = role.e;
     if (e >= n) return;
+#endif
+    if (w_final_exp_m(role, do_fe != 0)) return;
     const WL w = wl();
     const size_t stride = (size_t)plan.S * n;
     Fq<2> x = w_ld_split(g, stride, e, w);
 #pragma unroll 1
     for (int s = 1; s < plan.S; ++s) {
 #pragma unroll 1
-        for (int k = plan.lo[s]; k < plan.hi[s]; ++k) x = w12_mul(x, x);
+        for (int k = plan.lo[s]; k < plan.hi[s]; ++k) x = BN_WIDE_SQR ? w12_sqr(x) : w12_mul(x, x);
         x = w12_mul(x, w_ld_split(g, stride, (size_t)s * n + e, w));
     }
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (do_fe) {
         const bool zero = w12_is_zero(x);
-        if (zero && err && w.l == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
-        const Fq<2> r = w12_final_exp(x);
+        if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        const Fq<2> r = w_final_exp(role, x);
         if (!zero) fq_store_ref(r, words);
     } else {
         fq_store_ref(x, words);
     }
-    if (w.l < 12) st_words(&out[e].c[w_gt_index(w)], words);
+    if (w.l < 12 && live) st_words(&out[e].c[w_gt_index(w)], words);
 }
 
 // ---------------------------------------------------------------- k_pairing_latency
 // pairing() of a few pairs in ONE launch, for latency (bn_pairing_many_dev
 // batches of at most kLatencyMaxDefault pairs, capi.hip).  A block holds
-// kLatPairs pairs and three waves:
+// kLatPairs pairs and three waves (four with BN_FE_DUO):
 //  - wave 0, the producer: to_affine and the 87 line coefficients of each pair
 //    on eight lanes (lines_wide.h, as k_prepare_wide), each line scaled by P
 //    (ell_vw * Py, ell_vv * Px: mod.rs:589) and put into the pair's LDS ring;
@@ -126,7 +209,10 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
 //    on the wide layout (fq12_wide.h) right behind the producer -- per digit
 //    the generic square and the sparse product by each line as it arrives
 //    (mod.rs:579-607's order, so the Miller value is the reference's) -- then
-//    the final exponentiation (w12_final_exp), and stores the Gt image.
+//    the final exponentiation (w12_final_exp), and stores the Gt image;
+//  - BN_FE_DUO: the consumer is the squarer of the two-group final
+//    exponentiation (fq12_wide.h w12_final_exp_s); the multiplier groups are
+//    wave 0 once its lines are out (pairs 0-3) and wave 3 (pairs 4-7).
 // The loop needs no segments and no Horner recombination, and the three
 // kernels of the segmented latency path (k_prepare_wide, k_miller_seg,
 // k_horner_wide) become one.  Hand-off: the producer writes a line, waits for
@@ -136,6 +222,8 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
 // always progress, so every wave reaches the end; the spins are capped anyway.
 // (the ring itself, g_lat_ring, is declared in fq12_wide.h beside w12_mul_line)
 __shared__ uint32_t g_lat_prod[kLatPairs], g_lat_cons[kLatPairs], g_lat_skip[kLatPairs];
+__shared__ uint32_t g_lat_duo[kLatPairs * 4];  // BN_FE_DUO: the counters of each pair's channel
+static_assert(kDuoWords <= kLatRing * kLatLineWords, "the FE channel reuses the pair's line ring");
 constexpr uint32_t kLatSpinCap = 1u << 26;  // ~4 s of s_sleep 1: never reached while both sides run
 
 // Diagnostic build (-DBN_LAT_STAMPS=1, tools/lat_stamps.py): block 0 records
@@ -154,6 +242,21 @@ __device__ uint64_t g_lat_stamps[8];
 #define LAT_STAMP(cond, k) ((void)0)
 #endif
 
+#if BN_FE_DUO
+// the multiplier group of pair j (fq12_wide.h, two-group final exponentiation);
+// its channel is the pair's line ring, free once the Miller loop has read every
+// line -- before S hands over anything
+__device__ __forceinline__ void lat_multiplier(int j, size_t base, size_t n, const uint32_t* f_out) {
+#if BN_WIDE_PAD
+    if (f_out) return;  // no final exponentiation here (idle groups pair up with their idle squarers)
+#else
+    if (f_out || base + j >= n) return;  // no final exponentiation here / no pair
+#endif
+    WDuo duo = {g_lat_ring + j * kLatRing * kLatLineWords, g_lat_duo + 4 * j, 0, 0};
+    w12_final_exp_m(duo);
+}
+#endif
+
 // f_out != null (pairing_batch / miller_loop_batch): the Miller values go to
 // f_out (split layout, lane-strided, stride n; a zero-point pair's is one) for the
 // product reduction, and no final exponentiation runs here; mode 1
@@ -168,6 +271,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
         g_lat_cons[threadIdx.x] = 0;
         g_lat_skip[threadIdx.x] = 0;
     }
+    if (threadIdx.x < kLatPairs * 4) g_lat_duo[threadIdx.x] = 0;
     __syncthreads();
     volatile uint32_t* prod = g_lat_prod;
     volatile uint32_t* cons = g_lat_cons;
@@ -184,8 +288,12 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
         LAT_STAMP(threadIdx.x == 0, 1);  // producer: to_affine done
         if (st && c == 0) g_lat_skip[j] = a.skip ? 1u : 0u;
         auto emit = [&](int line, const Ell& e) {
-            const auto x4 = narrow<kLine>(fq2_scale(e.ell_vw, a.py));
-            const auto x2 = narrow<kLine>(fq2_scale(e.ell_vv, a.px));
+            // slots 0, 2 scale ell_vw by Py, slots 1, 3 ell_vv by Px (one product
+            // per lane instead of two); slot 0 takes x2 from slot 1
+            const bool odd_slot = (k & 1) != 0;
+            const auto y = narrow<kLine>(fq2_scale(fq2_select(odd_slot, e.ell_vv, e.ell_vw), fq_select(odd_slot, a.px, a.py)));
+            const auto x4 = y;
+            const auto x2 = pw_from(y, 1);
             for (uint32_t spins = 0; BN_ANY(valid && line - (int)cons[j] >= kLatRing) && spins < kLatSpinCap; ++spins)
                 __builtin_amdgcn_s_sleep(1);
             asm volatile("" ::: "memory");
@@ -221,12 +329,30 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
         emit(line++, pw_mixed_addition_step(r, q1, k));
         emit(line++, pw_mixed_addition_step(r, q2, k));
         LAT_STAMP(threadIdx.x == 0, 2);  // producer: last line out
+#if BN_FE_DUO
+        lat_multiplier((int)threadIdx.x / kWLanes, base, n, f_out);
+#endif
         return;
     }
+#if BN_FE_DUO
+    if (threadIdx.x >= 64 + kLatPairs * kWLanes) {  // wave 3: the multipliers of pairs 4-7
+        lat_multiplier(kLatPairs / 2 + ((int)threadIdx.x - 64 - kLatPairs * kWLanes) / kWLanes, base, n, f_out);
+        return;
+    }
+#endif
     // ---- consumer groups: pair j on a 16-lane group of waves 1-2
     const int j = ((int)threadIdx.x - 64) / kWLanes;
+#if BN_WIDE_PAD
+    // idle groups repeat the block's last pair (the producer fills their rings
+    // with it) and store nothing, so a wave runs the same number of groups
+    // whatever n is
+    const bool live = base + j < n;
+    const size_t pi = live ? base + j : n - 1;
+#else
+    const bool live = true;
     const size_t pi = base + j;
     if (pi >= n) return;
+#endif
     const WL w = wl();
     auto ln = [&](int line) { return (uint32_t)((j * kLatRing + line % kLatRing) * kLatLineWords); };
     auto wait_line = [&](int line) {
@@ -245,7 +371,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
 #pragma unroll 1
     for (int d = 0; d < BN_NAF_DIGITS; ++d) {
         if (d > 0) {
-            f = w12_mul(f, f);  // the generic square, as the reference's loop
+            f = BN_WIDE_SQR ? w12_sqr(f) : w12_mul(f, f);  // the generic square, as the reference's loop
             wait_line(line);
             f = w12_mul_line(f, ln(line));
             took(line++);
@@ -267,16 +393,21 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
     const Fq<2> one = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
     const Fq<2> x = g_lat_skip[j] ? one : f;
     if (f_out) {  // the Miller value, for the product of pairing_batch / miller_loop_batch
-        w_st_split(f_out, n, pi, w, x);
+        if (live) w_st_split(f_out, n, pi, w, x);
         return;
     }
     const bool zero = w12_is_zero(x);
-    if (zero && err && w.l == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+    if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+#if BN_FE_DUO
+    WDuo duo = {g_lat_ring + j * kLatRing * kLatLineWords, g_lat_duo + 4 * j, 0, 0};
+    const Fq<2> res = w12_final_exp_s(x, duo);
+#else
     const Fq<2> res = w12_final_exp(x);
+#endif
     LAT_STAMP(threadIdx.x == 64, 5);  // consumer: final exponentiation done
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!zero) fq_store_ref(res, words);
-    if (w.l < 12) st_words(&out[pi].c[w_gt_index(w)], words);
+    if (w.l < 12 && live) st_words(&out[pi].c[w_gt_index(w)], words);
 }
 
 // *status = the bn_status of the device-side outcome bits in *err (bn_*_batch_dev)

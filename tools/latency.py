@@ -40,6 +40,8 @@ def main():
                     help="batches up to this size take the latency path (bn_set_fe_wide_max)")
     ap.add_argument("--latency-max", type=int, default=None,
                     help="latency-path batches up to this size run k_pairing_latency (bn_set_latency_max)")
+    ap.add_argument("--warm-ms", type=float, default=100.0,
+                    help="repeat each call this long before timing it (the GPU clock ramps up under load)")
     args = ap.parse_args()
     import torch
 
@@ -87,7 +89,10 @@ def main():
                 def fn():
                     ctx.pairing_many_dev(P.data_ptr(), Q.data_ptr(), n, out.data_ptr(), sh)
                     stream.synchronize()
+            t_end = time.perf_counter() + args.warm_ms * 1e-3
             fn()
+            while time.perf_counter() < t_end:
+                fn()
             dt = med(fn, args.reps)
             print(json.dumps({"call": call, "n": n, "ms": dt * 1e3, "per_item_us": dt / n * 1e6,
                               "cpu_1thread_ms": cpu1 * n * 1e3, "fe_wide_max": args.fe_wide_max,
