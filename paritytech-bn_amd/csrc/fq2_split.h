@@ -143,6 +143,36 @@ BN_INLINE Fq<kenc(kv(K) + 1, sub_spread(kl(K)) + 2)> fq_neg_lazy(const Fq<K>& x)
     for (int i = 0; i < 9; ++i) r.v[i] = Q.v[i] - x.v[i];
     return r;
 }
+// 1: fq2_mul_split takes its w operand (lane 0: K*p - b1, lane 1: b1) as one
+// v_cndmask_b32_dpp per digit -- odd lanes keep their own b1, even lanes take the
+// partner's K*p - b1 through the DPP swap -- instead of a broadcast, a negation
+// and a select (A/B; 2: VCC written by a VALU compare instead of SALU moves)
+#ifndef BN_FQ2_DPPSEL
+#define BN_FQ2_DPPSEL 0
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_DPPSEL
+#if BN_FQ2_DPPSEL == 2
+#define BN_DPPSEL_VCC "v_cmp_ne_u32_e32 vcc, 0, %27\n\ts_nop 1\n\t"
+#else
+#define BN_DPPSEL_VCC "s_mov_b32 vcc_lo, 0xaaaaaaaa\n\ts_mov_b32 vcc_hi, 0xaaaaaaaa\n\ts_nop 1\n\t"
+#endif
+#define BN_DPPSEL_OP(o, a, b) "v_cndmask_b32_dpp %" #o ", %" #a ", %" #b ", vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+// w[i] = odd lane ? own[i] : the partner's neg[i].  The s_nop covers the two
+// wait states a DPP read needs after the VALU write of its source (the hazard
+// recognizer does not look inside inline asm).
+BN_INLINE void dpp_sel_own_partner(uint32_t (&w)[9], const uint32_t (&own)[9], const uint32_t (&neg)[9]) {
+    const uint32_t odd = __builtin_amdgcn_workitem_id_x() & 1u;
+    asm(BN_DPPSEL_VCC BN_DPPSEL_OP(0, 9, 18) BN_DPPSEL_OP(1, 10, 19) BN_DPPSEL_OP(2, 11, 20) BN_DPPSEL_OP(3, 12, 21)
+            BN_DPPSEL_OP(4, 13, 22) BN_DPPSEL_OP(5, 14, 23) BN_DPPSEL_OP(6, 15, 24) BN_DPPSEL_OP(7, 16, 25)
+                BN_DPPSEL_OP(8, 17, 26)
+        : "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6]), "=&v"(w[7]),
+          "=&v"(w[8])
+        : "v"(neg[0]), "v"(neg[1]), "v"(neg[2]), "v"(neg[3]), "v"(neg[4]), "v"(neg[5]), "v"(neg[6]), "v"(neg[7]),
+          "v"(neg[8]), "v"(own[0]), "v"(own[1]), "v"(own[2]), "v"(own[3]), "v"(own[4]), "v"(own[5]), "v"(own[6]),
+          "v"(own[7]), "v"(own[8]), "v"(odd)
+        : "vcc");
+}
+#endif
 // per-lane choice between two values of different static types (the join)
 template <int A, int B>
 BN_INLINE Fq<kjoin(A, B)> fq_pick(bool c, const Fq<A>& a, const Fq<B>& b) {
@@ -203,7 +233,13 @@ BN_INLINE auto fq2_mul_split(const Fq2<A>& a, const Fq2<B>& b) {
     } else {
         const bool odd = lane_odd();
         const Fq<A> pa = fq_partner(a.c);
-#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_BCAST
+#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_DPPSEL
+        const Fq<B> y = fq_bcast_c0(b.c);
+        const auto nb = fq_neg_lazy(b.c);  // the odd lane's is K*p - b1
+        Fq<kjoin(B, kenc(kv(B) + 1, sub_spread(kl(B)) + 2))> w;
+        dpp_sel_own_partner(w.v, b.c.v, nb.v);
+        (void)odd;
+#elif defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_BCAST
         // y = b0 and c1 = b1 on both lanes straight from DPP (no select for y)
         const Fq<B> y = fq_bcast_c0(b.c);
         const Fq<B> c1 = fq_bcast_c1(b.c);

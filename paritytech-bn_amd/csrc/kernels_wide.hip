@@ -162,9 +162,24 @@ __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __r
 // loop squares its accumulator), then the final exponentiation when do_fe
 // (pairing / pairing_batch; zero -> zero image + error bit) or the Miller value
 // itself (miller_loop_batch) -> out[e].
+#ifndef BN_LAT_STAMPS
+#define BN_LAT_STAMPS 0
+#endif
+#if BN_LAT_STAMPS
+// diagnostic build: block 0's group 0 stamps s_memrealtime (100 MHz) at the
+// phase boundaries of k_horner_wide (tools/lat_stamps.py --horner)
+__device__ uint64_t g_hor_stamps[8];
+#define HOR_STAMP(k)                                                                       \
+    do {                                                                                   \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_hor_stamps[k] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define HOR_STAMP(k) ((void)0)
+#endif
 __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, size_t n, SegPlan plan,
                                                         int do_fe, bn_gt* __restrict__ out, int* __restrict__ err,
                                                         int duo) {
+    HOR_STAMP(0);  // start
     fold_table_init();
     w_duo_init();
     const WRole role = w_role(duo != 0);
@@ -180,17 +195,22 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
     const WL w = wl();
     const size_t stride = (size_t)plan.S * n;
     Fq<2> x = w_ld_split(g, stride, e, w);
+    HOR_STAMP(1);  // g_0 in
 #pragma unroll 1
     for (int s = 1; s < plan.S; ++s) {
 #pragma unroll 1
         for (int k = plan.lo[s]; k < plan.hi[s]; ++k) x = BN_WIDE_SQR ? w12_sqr(x) : w12_mul(x, x);
+        if (s == 1) HOR_STAMP(2);  // the first run of squarings
         x = w12_mul(x, w_ld_split(g, stride, (size_t)s * n + e, w));
+        if (s == 1) HOR_STAMP(3);  // its load + product
     }
+    HOR_STAMP(4);  // recombination done
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (do_fe) {
         const bool zero = w12_is_zero(x);
         if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
         const Fq<2> r = w_final_exp(role, x);
+        HOR_STAMP(5);  // final exponentiation done
         if (!zero) fq_store_ref(r, words);
     } else {
         fq_store_ref(x, words);
@@ -423,5 +443,8 @@ __global__ void __launch_bounds__(kBlock) k_err_status(const int* __restrict__ e
 #if BN_LAT_STAMPS
 extern "C" int bn_dbg_lat_stamps(uint64_t out[8]) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(bn::g_lat_stamps), 8 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+extern "C" int bn_dbg_hor_stamps(uint64_t out[8]) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(bn::g_hor_stamps), 8 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
 }
 #endif

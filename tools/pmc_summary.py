@@ -70,18 +70,29 @@ for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
 # read calibration on k_fe_out (n pairings: 2 * 432 + 1 bytes read, 384 written)
 cal = agg.get("k_fe_out", {})
 read_factor, write_factor = None, None
+factor_src = tag
+prev = os.path.join(out_dir, "pmc_summary.json")
 if cal.get("FETCH_SIZE") and cal.get("WRITE_SIZE"):
     n_cal = 65536  # bench.py's default batch (pairs per GPU)
     read_factor = (sum(cal["FETCH_SIZE"]) / len(cal["FETCH_SIZE"]) * 1024) / (n_cal * (2 * 432 + 1))
     write_factor = (sum(cal["WRITE_SIZE"]) / len(cal["WRITE_SIZE"]) * 1024) / (n_cal * 384)
     print("calibration on k_fe_out: FETCH_SIZE/expected reads = %.3f, WRITE_SIZE/expected writes = %.3f"
           % (read_factor, write_factor))
+elif os.path.exists(prev):
+    # the default build runs the whole pairing in k_pairing_full, so no k_fe_out to calibrate
+    # on: keep the factor of the last session that had one (the same access pattern)
+    for v in json.load(open(prev)).values():
+        if v.get("read_factor"):
+            read_factor, write_factor = v["read_factor"], v.get("write_factor")
+            factor_src = v.get("read_factor_source", "an earlier session")
+            break
+    print("read factor %s from %s (no k_fe_out in this session)" % (read_factor, factor_src))
 summary = {}
 # SURVEY.md 8(d) generic Fq-mul counts per element of the bench's kernels, and how many
 # elements one wave carries (the pairing path runs two lanes per pairing)
-ALG_FQMUL = {"k_pairing_fused": 19 + 2655 + 6045, "k_prepare": 19 + 2655, "k_miller": 6045, "k_fq12_vm": 8767,
+ALG_FQMUL = {"k_pairing_full": 19 + 2655 + 6045 + 8767, "k_pairing_fused": 19 + 2655 + 6045, "k_prepare": 19 + 2655, "k_miller": 6045, "k_fq12_vm": 8767,
              "k_g1_mul": 3800, "k_g2_mul": 9165}
-ELEMS_PER_WAVE = {"k_pairing_fused": 32, "k_prepare": 32, "k_miller": 32, "k_fq12_vm": 32, "k_fe_out": 32}
+ELEMS_PER_WAVE = {"k_pairing_full": 32, "k_pairing_fused": 32, "k_prepare": 32, "k_miller": 32, "k_fq12_vm": 32, "k_fe_out": 32}
 lines = ["%-16s %14s %14s %14s %12s %10s" % ("kernel", "FETCH_bytes", "WRITE_bytes", "VALU/wave", "WAVE_CYC/w",
                                                  "VALU/cyc")]
 for k, v in sorted(agg.items()):
@@ -100,7 +111,7 @@ for k, v in sorted(agg.items()):
     per_wave = ELEMS_PER_WAVE.get(k, 64)
     valu_per_mad = valu * 64 / per_wave / (alg * 128) if alg else None
     summary[k] = {"hbm_bytes_per_launch": corr, "fetch_bytes_raw": fetch, "write_bytes": write,
-                  "read_factor": read_factor, "write_factor": write_factor,
+                  "read_factor": read_factor, "write_factor": write_factor, "read_factor_source": factor_src,
                   "valu_insts_per_wave": valu, "wave_cycles": cyc,
                   "valu_per_cycle_per_wave": valu / cyc if cyc else None,
                   "algorithmic_fqmul_per_element": alg, "elements_per_wave": per_wave,
@@ -115,7 +126,8 @@ for k, v in sorted(agg.items()):
                                       for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
                                                 "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_MISC")
                                       if c in m},
-                  "note": "FETCH_SIZE corrected by the read factor calibrated on k_fe_out (known bytes), "
+                  "note": "FETCH_SIZE corrected by the read factor calibrated on k_fe_out (known bytes, session "
+                          + factor_src + "), "
                           "WRITE_SIZE as counted (MI355X_MICROARCH §HBM); source %s" % tag}
     lines.append("%-16s %14.3e %14.3e %14.3e %12.3e %10.3f" % (k, fetch, write, valu, cyc, valu / cyc if cyc else 0))
 if summary:
