@@ -433,15 +433,30 @@ int chunk_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int m
 uint32_t* parts_region(bn_ctx* c, size_t nchunks) {
     return nchunks == 1 ? slot_region(c, kRegionResult) : slot_region(c, kRegionParts);
 }
+// the S segment values of ONE product (result region, element s, stride S) ->
+// their recombination, then the final exponentiation (do_fe) or the Miller value,
+// into *d_out: k_horner_tree (the squarings of the segments side by side and a
+// product tree); BN254MI_HORNER_TREE=0 selects k_horner_wide (one group, Horner's
+// rule), kept for A/B
+static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out, hipStream_t s) {
+    const char* env = getenv("BN254MI_HORNER_TREE");
+    const bool tree = !(env && env[0] == '0');
+    if (tree)
+        k_horner_tree<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err,
+                                           wide_duo(1) ? 1 : 0);
+    else
+        k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, plan, do_fe, d_out, c->d_err,
+                                           wide_duo(1) ? 1 : 0);
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
 // per segment, the chunk partials -> the result region; then the Horner
 // recombination (+ the final exponentiation for pairing_batch) into *d_out
 int finish_product(bn_ctx* c, const SegPlan& plan, size_t nchunks, int do_fe, bn_gt* d_out, hipStream_t s) {
     if (nchunks > 1)
         RET_IF(product_wide(c, slot_region(c, kRegionParts), plan.S * nchunks, nchunks, nchunks, plan.S,
                             slot_region(c, kRegionResult), plan.S, 0, 1, s));
-    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, plan, do_fe, d_out, c->d_err, wide_duo(1) ? 1 : 0);
-    HIPCHK(c, hipGetLastError());
-    return BN_OK;
+    return recombine_one(c, plan, do_fe, d_out, s);
 }
 // The product of n <= c->latency_max device pairs: their Miller values from the
 // one-launch k_pairing_latency (no FE), the product reduction, then one group's
@@ -454,10 +469,7 @@ int latency_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int
         d_p, d_q, n, nullptr, slot_region(c, kRegionSeg), mode, c->d_err);
     HIPCHK(c, hipGetLastError());
     RET_IF(product_wide(c, slot_region(c, kRegionSeg), n, n, n, 1, slot_region(c, kRegionResult), 1, 0, 1, s));
-    const SegPlan whole = cut_plan(1, 1);  // one segment: x = the product, then the FE when do_fe
-    k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, whole, do_fe, d_out, c->d_err, wide_duo(1) ? 1 : 0);
-    HIPCHK(c, hipGetLastError());
-    return BN_OK;
+    return recombine_one(c, cut_plan(1, 1), do_fe, d_out, s);  // one segment: the FE of the product when do_fe
 }
 bool use_latency_product(const bn_ctx* c, size_t n) { return n <= c->latency_max && n <= c->fe_wide_max; }
 

@@ -380,13 +380,16 @@ __device__ __noinline__ Fq<2> w12_exp_by_neg_z(Fq<2> x) {
     return w12_conj(r);
 }
 
-// final_exponentiation (fq12.rs:107-110) of a nonzero f: first chunk
-// (fq12.rs:62-73) and last chunk (fq12.rs:75-105) in the reference's order
-__device__ __noinline__ Fq<2> w12_final_exp(Fq<2> f) {
+// the first chunk of the final exponentiation (fq12.rs:62-73) of a nonzero f:
+// f^((p^6 - 1)(p^2 + 1)), an element of the cyclotomic subgroup
+__device__ __noinline__ Fq<2> w12_fe_first(Fq<2> f) {
     const Fq<2> b0 = w12_inv(f);
     const Fq<2> c0 = w12_mul(w12_conj(f), b0);
     const Fq<2> d0 = w12_frob<2>(c0);
-    const Fq<2> s = w12_mul(d0, c0);
+    return w12_mul(d0, c0);
+}
+// its last chunk (fq12.rs:75-105) of s = w12_fe_first(f)
+__device__ __noinline__ Fq<2> w12_fe_last(Fq<2> s) {
     const Fq<2> a = w12_exp_by_neg_z(s);
     const Fq<2> b = w12_cyc(a);
     const Fq<2> c = w12_cyc(b);
@@ -407,6 +410,9 @@ __device__ __noinline__ Fq<2> w12_final_exp(Fq<2> f) {
     const Fq<2> u = w12_frob<3>(t);
     return w12_mul(u, r);
 }
+// final_exponentiation (fq12.rs:107-110) of a nonzero f: first chunk and last
+// chunk in the reference's order
+__device__ __forceinline__ Fq<2> w12_final_exp(const Fq<2>& f) { return w12_fe_last(w12_fe_first(f)); }
 
 
 // ---------------------------------------------------------------- two-group final exponentiation
@@ -508,15 +514,12 @@ __device__ __noinline__ Fq<2> w12_exp_mul(WDuo& d) {
     d.put_result(w12_conj(acc));
     return x;
 }
-// final_exponentiation (fq12.rs:107-110) of f on S; returns the result on S.
+// The last chunk of the final exponentiation (fq12.rs:75-105) of s =
+// w12_fe_first(f) on S; returns the result on S.
 // The hand-overs: [24 powers of s], b, [24 powers of d], [24 powers of f1], k.
 // M returns a, e, g and then o = frob(k*b), u = frob^3(conj(s)*k*b) while S
 // forms m, n and q (the reference's names, fq12.rs:75-105).
-__device__ __noinline__ Fq<2> w12_final_exp_s(Fq<2> f, WDuo& d) {
-    const Fq<2> b0 = w12_inv(f);
-    const Fq<2> c0 = w12_mul(w12_conj(f), b0);
-    const Fq<2> d0 = w12_frob<2>(c0);
-    const Fq<2> s = w12_mul(d0, c0);
+__device__ __noinline__ Fq<2> w12_fe_last_s(Fq<2> s, WDuo& d) {
     const Fq<2> a = w12_exp_sq(s, d);
     const Fq<2> b = w12_cyc(a);
     d.put(b);
@@ -537,6 +540,8 @@ __device__ __noinline__ Fq<2> w12_final_exp_s(Fq<2> f, WDuo& d) {
     const Fq<2> u = d.get_result();
     return w12_mul(u, r);
 }
+// final_exponentiation (fq12.rs:107-110) of f on S (first chunk, then the last on S and M)
+__device__ __forceinline__ Fq<2> w12_final_exp_s(const Fq<2>& f, WDuo& d) { return w12_fe_last_s(w12_fe_first(f), d); }
 // M's part of the same final exponentiation
 __device__ __noinline__ void w12_final_exp_m(WDuo& d) {
     const Fq<2> s = w12_exp_mul(d);  // a

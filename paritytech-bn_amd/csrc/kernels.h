@@ -519,6 +519,10 @@ __global__ void __launch_bounds__(kPairBlock) k_miller_seg(const uint32_t* __res
 // exponentiation when do_fe
 __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restrict__ g, size_t n, SegPlan plan,
                                                         int do_fe, bn_gt* __restrict__ out, int* __restrict__ err, int duo);
+// the same for ONE element (n = 1) on the S groups of one block: group s raises g_s
+// to 2^(len_(s+1) + ... + len_(S-1)), then a product tree; out[0]
+__global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restrict__ g, SegPlan plan, int do_fe,
+                                                        bn_gt* __restrict__ out, int* __restrict__ err, int duo);
 __global__ void __launch_bounds__(kPairBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
                           uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
                           int* __restrict__ err, int mode);

@@ -73,6 +73,17 @@ __device__ __forceinline__ Fq<2> w_final_exp(const WRole& r, const Fq<2>& x) {
     (void)r;
     return w12_final_exp(x);
 }
+// the last chunk only, of s = w12_fe_first(x) (k_horner_tree)
+__device__ __forceinline__ Fq<2> w_fe_last(const WRole& r, const Fq<2>& s) {
+#if BN_FE_DUO
+    if (r.duo) {
+        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0};
+        return w12_fe_last_s(s, d);
+    }
+#endif
+    (void)r;
+    return w12_fe_last(s);
+}
 // M's part; true if this group is M (and has done it)
 __device__ __forceinline__ bool w_final_exp_m(const WRole& r, bool run) {
 #if BN_FE_DUO
@@ -216,6 +227,94 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
         fq_store_ref(x, words);
     }
     if (w.l < 12 && live) st_words(&out[e].c[w_gt_index(w)], words);
+}
+
+// The same recombination for ONE element (n = 1: the product of pairing_batch /
+// miller_loop_batch) on the S <= 16 groups of one block, as a tree.  Horner's
+// value f = (..(g_0^(2^len_1) g_1)^(2^len_2)..)^(2^len_(S-1)) g_(S-1) is the
+// product over s of g_s^(2^e_s), e_s = len_(s+1) + .. + len_(S-1), because
+// squaring is a ring homomorphism; so group s loads g_s and squares it e_s times,
+// and the sixteen values are multiplied in a tree through LDS (Fq12
+// multiplication is commutative and associative).  The dependent chain is group
+// 0's e_0 squarings and four products, instead of the same squarings, S - 1
+// products and S - 1 global loads one after another.
+// pairing_batch (do_fe): the first chunk of the final exponentiation E1(x) =
+// x^((p^6 - 1)(p^2 + 1)) is a power map, so E1(f) = prod E1(g_s)^(2^e_s).  Every
+// group runs E1 on its g_s (side by side) and then squares in the cyclotomic
+// subgroup (Granger-Scott, w12_cyc: the same square as the generic one there, at
+// about half its instructions); group 0 then runs only the last chunk, so the
+// final exponentiation's value is the reference's.  f = 0 iff some g_s = 0 (a
+// field), which sets the error bit and the zero image as before.
+// miller_loop_batch: generic squarings and the Miller value itself.
+// Every group of the block stays busy to the end (a wave whose other groups have
+// returned runs its last group markedly slower): groups past S work
+// on one, every group runs group 0's number of squarings and keeps its own
+// count's result, every group computes each tree level's product and keeps it
+// where the level needs it, and the last chunk then runs on every group pair --
+// S groups 0-7 with M groups 8-15 (BN_FE_DUO) -- on copies of group 0's value;
+// group 0 stores the result.
+__shared__ uint32_t g_hor_zero;
+__global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restrict__ g, SegPlan plan, int do_fe,
+                                                        bn_gt* __restrict__ out, int* __restrict__ err, int duo) {
+    HOR_STAMP(0);  // start
+    if (threadIdx.x == 0) g_hor_zero = 0;
+    fold_table_init();
+    w_duo_init();
+    const WL w = wl();
+    const int grp = (int)threadIdx.x / kWLanes;
+    const bool seg = grp < plan.S;
+    Fq<2> x = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
+    if (seg) x = w_ld_split(g, (size_t)plan.S, (size_t)grp, w);
+    int e = 0, e0 = 0;  // this group's squarings (g_s^(2^e_s)) and group 0's (the most)
+    for (int t = 1; t < plan.S; ++t) {
+        e0 += plan.hi[t] - plan.lo[t];
+        if (t > grp) e += plan.hi[t] - plan.lo[t];
+    }
+    HOR_STAMP(1);  // g_0 in
+    if (do_fe) {
+        if (seg && w12_is_zero(x) && w.l == 0) g_hor_zero = 1;
+        x = w12_fe_first(x);  // first chunk; of one (groups past S): one
+        HOR_STAMP(3);         // group 0's first chunk done
+#pragma unroll 1
+        for (int k = 0; k < e0; ++k) {
+            const Fq<2> y = w12_cyc(x);
+            x = k < e ? y : x;
+        }
+    } else {
+#pragma unroll 1
+        for (int k = 0; k < e0; ++k) {
+            const Fq<2> y = BN_WIDE_SQR ? w12_sqr(x) : w12_mul(x, x);
+            x = k < e ? y : x;
+        }
+    }
+    HOR_STAMP(2);  // group 0's squarings done
+    uint32_t* mine = g_wval + (grp * kWLanes) * kWSlot;
+#pragma unroll 1
+    for (int h = kWGroups / 2; h >= 1; h /= 2) {
+        w_put(mine, w.l, x);
+        __syncthreads();
+        const Fq<2> y = w12_mul(x, w_get<2>(g_wval + (((grp + h) % kWGroups) * kWLanes) * kWSlot, w.l));
+        if (grp < h && grp + h < plan.S) x = y;  // groups past S hold one
+        __syncthreads();
+    }
+    // every group takes group 0's value: the pairs (g, g + 8) run the last chunk side by side
+    if (grp == 0) w_put(g_wval, w.l, x);
+    __syncthreads();
+    x = w_get<2>(g_wval, w.l);
+    HOR_STAMP(4);  // recombination done
+    const WRole role = w_role(duo != 0);  // group g < 8: S of channel g; group g + 8: its M
+    if (w_final_exp_m(role, do_fe != 0)) return;
+    uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (do_fe) {
+        const bool zero = g_hor_zero != 0;
+        if (zero && err && w.l == 0 && grp == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        const Fq<2> r = w_fe_last(role, x);
+        HOR_STAMP(5);  // final exponentiation done
+        if (!zero) fq_store_ref(r, words);
+    } else {
+        fq_store_ref(x, words);
+    }
+    if (w.l < 12 && grp == 0) st_words(&out[0].c[w_gt_index(w)], words);
 }
 
 // ---------------------------------------------------------------- k_pairing_latency
