@@ -70,7 +70,13 @@ template <int X>
 BN_INLINE LineOps line_ops(const Fq2<X>& v_in) {
     const Fq<kv(X)> v = fq_norm(v_in.c);
     const bool odd = lane_odd();
-#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_BCAST
+#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_DPPSEL
+    // w as fq2_mul_split forms it: the odd lane's own v1, the even lane the partner's K*p - v1
+    Fq<kjoin(kv(X), kenc(kv(X) + 1, 2))> w;
+    dpp_sel_own_partner(w.v, v.v, fq_neg_lazy(v).v);
+    (void)odd;
+    return {widen<kLine>(fq_bcast_c0(v)), widen<8>(fq_norm(w))};
+#elif defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_BCAST
     const Fq<kv(X)> c1 = fq_bcast_c1(v);
     return {widen<kLine>(fq_bcast_c0(v)), widen<8>(fq_norm(fq_pick(odd, c1, fq_neg_lazy(c1))))};
 #else
