@@ -43,7 +43,9 @@ typedef enum {
     BN_ERR_TO_AFFINE = 2,     /* CurveError::ToAffineConversion (lib.rs:629-630) */
     BN_ERR_FE_ZERO = 3,       /* final exponentiation of zero: fq12.rs:63-72 None; pairing panics (mod.rs:900) */
     BN_ERR_HIP = 4,           /* a HIP runtime error; see bn_last_error() */
-    BN_ERR_NO_DEVICE = 5
+    BN_ERR_NO_DEVICE = 5,
+    BN_ERR_INTERNAL = 6       /* a device-side hand-off between waves ran out of its wait cap; the result is
+                                 not trusted and the call fails (never seen in normal operation) */
 } bn_status;
 
 typedef struct bn_ctx bn_ctx;
@@ -58,6 +60,12 @@ int bn_ctx_destroy(bn_ctx* ctx);
 const char* bn_last_error(const bn_ctx* ctx);
 /* the stream *_dev calls use when given NULL */
 void* bn_ctx_stream(bn_ctx* ctx);
+/* The sticky device outcome of the *_dev calls without a status word (bn_pairing_many_dev,
+ * bn_pairing_many_allgather_dev): synchronizes `stream` (NULL: the context's stream), returns
+ * BN_ERR_INTERNAL or BN_ERR_FE_ZERO (a Miller value was zero: the reference panics, mod.rs:900)
+ * if any such call since the last bn_dev_status (or host-buffer call, which starts from a clear
+ * word) set it, else BN_OK, and clears it.  On a multi-device context it checks every device. */
+int bn_dev_status(bn_ctx* ctx, void* stream);
 
 /* ---- several devices of the node in one process ----
  * A multi-device context shards the host-buffer calls bn_pairing_many,
@@ -132,6 +140,36 @@ int bn_g1_mul_many_dev(bn_ctx* ctx, const bn_g1* d_p, const bn_fr* d_k, size_t n
 int bn_g2_mul_many(bn_ctx* ctx, const bn_g2* p, const bn_fr* k, size_t n, bn_g2* out);
 int bn_g2_mul_many_dev(bn_ctx* ctx, const bn_g2* d_p, const bn_fr* d_k, size_t n, bn_g2* d_out, void* stream);
 
+/* ---- group law (lib.rs:388-423, 539-574; src/groups/mod.rs:169-216, 294-358) ----
+ * Batched forms of the G1 / G2 operators, each lane running the reference's own
+ * Jacobian formulas, so the output images are bit-identical (not merely equal points):
+ *   add        out = a + b      (mod.rs:294-334: both zero shortcuts, the doubling when a == b)
+ *   sub        out = a - b      (mod.rs:352-358: a + (-b))
+ *   neg        out = -a         (mod.rs:336-350: zero unchanged, else (x, -y, z))
+ *   normalize  out = a.normalize() (lib.rs:391-398: to_affine then to_jacobian, z = one,
+ *              mod.rs:199-226; zero unchanged)
+ *   eq         eq[i] = (a == b) (PartialEq, mod.rs:169-195: projective equality) as 0 / 1 */
+int bn_g1_add_many(bn_ctx* ctx, const bn_g1* a, const bn_g1* b, size_t n, bn_g1* out);
+int bn_g1_sub_many(bn_ctx* ctx, const bn_g1* a, const bn_g1* b, size_t n, bn_g1* out);
+int bn_g1_neg_many(bn_ctx* ctx, const bn_g1* a, size_t n, bn_g1* out);
+int bn_g1_normalize_many(bn_ctx* ctx, const bn_g1* a, size_t n, bn_g1* out);
+int bn_g1_eq_many(bn_ctx* ctx, const bn_g1* a, const bn_g1* b, size_t n, uint8_t* eq);
+int bn_g2_add_many(bn_ctx* ctx, const bn_g2* a, const bn_g2* b, size_t n, bn_g2* out);
+int bn_g2_sub_many(bn_ctx* ctx, const bn_g2* a, const bn_g2* b, size_t n, bn_g2* out);
+int bn_g2_neg_many(bn_ctx* ctx, const bn_g2* a, size_t n, bn_g2* out);
+int bn_g2_normalize_many(bn_ctx* ctx, const bn_g2* a, size_t n, bn_g2* out);
+int bn_g2_eq_many(bn_ctx* ctx, const bn_g2* a, const bn_g2* b, size_t n, uint8_t* eq);
+int bn_g1_add_many_dev(bn_ctx* ctx, const bn_g1* d_a, const bn_g1* d_b, size_t n, bn_g1* d_out, void* stream);
+int bn_g1_sub_many_dev(bn_ctx* ctx, const bn_g1* d_a, const bn_g1* d_b, size_t n, bn_g1* d_out, void* stream);
+int bn_g1_neg_many_dev(bn_ctx* ctx, const bn_g1* d_a, size_t n, bn_g1* d_out, void* stream);
+int bn_g1_normalize_many_dev(bn_ctx* ctx, const bn_g1* d_a, size_t n, bn_g1* d_out, void* stream);
+int bn_g1_eq_many_dev(bn_ctx* ctx, const bn_g1* d_a, const bn_g1* d_b, size_t n, uint8_t* d_eq, void* stream);
+int bn_g2_add_many_dev(bn_ctx* ctx, const bn_g2* d_a, const bn_g2* d_b, size_t n, bn_g2* d_out, void* stream);
+int bn_g2_sub_many_dev(bn_ctx* ctx, const bn_g2* d_a, const bn_g2* d_b, size_t n, bn_g2* d_out, void* stream);
+int bn_g2_neg_many_dev(bn_ctx* ctx, const bn_g2* d_a, size_t n, bn_g2* d_out, void* stream);
+int bn_g2_normalize_many_dev(bn_ctx* ctx, const bn_g2* d_a, size_t n, bn_g2* d_out, void* stream);
+int bn_g2_eq_many_dev(bn_ctx* ctx, const bn_g2* d_a, const bn_g2* d_b, size_t n, uint8_t* d_eq, void* stream);
+
 /* ---- Gt / Fq12 element operations (src/fields/fq12.rs) for batched callers and tests ---- */
 typedef enum {
     BN_FQ12_MUL = 0,          /* a * b          fq12.rs:319-327 (Gt * Gt, lib.rs:603-609) */
@@ -197,11 +235,12 @@ int bn_gt_pow_many_dev(bn_ctx* ctx, const bn_gt* d_a, const bn_fr* d_k, size_t n
 /* enable HIP-event timing of each kernel phase of bn_pairing_many_dev (events are
  * recorded on the launch stream between the kernels) */
 int bn_set_phase_timing(bn_ctx* ctx, int enable);
-/* Batches of at most n elements take the latency path: bn_pairing_many_dev runs the
- * Miller loop in segments and the recombination + final exponentiation on 16-lane
- * groups, bn_final_exponentiation_many the 16-lane final exponentiation
- * (kernels_wide.hip); larger batches take the throughput path (k_pairing_fused +
- * the two-lane step machine k_fq12_vm).  Default 8192 (the measured crossover) or
+/* Batches of at most n elements take the latency path: bn_pairing_many_dev runs
+ * k_pairing_latency (up to bn_set_latency_max pairs) or the segmented Miller loop with
+ * the recombination + final exponentiation on 16-lane groups, bn_final_exponentiation_many
+ * the 16-lane final exponentiation (kernels_wide.hip); larger batches take the throughput
+ * path (k_pairing_full: to_affine, lines, Miller loop and the two-lane final-exponentiation
+ * step machine in one launch).  Default 8192 (the measured crossover) or
  * $BN254MI_FE_WIDE_MAX; results are identical either way.  On a multi-device
  * context it applies to every device. */
 int bn_set_fe_wide_max(bn_ctx* ctx, size_t n);
@@ -211,9 +250,12 @@ int bn_set_fe_wide_max(bn_ctx* ctx, size_t n);
  * the final exponentiation); larger ones the segmented three-kernel form.
  * Default 2048 or $BN254MI_LATENCY_MAX; 0 disables it; results are identical. */
 int bn_set_latency_max(bn_ctx* ctx, size_t n);
-/* device milliseconds per phase since the last read: ms[0] k_prepare (to_affine +
- * G2 lines), ms[1] k_miller, ms[2] final exponentiation (k_fq12_vm, or k_fe_wide for
- * batches up to the wide threshold), ms[3] k_fe_out (0 with k_fe_wide);
+/* device milliseconds per phase of bn_pairing_many_dev since the last read, per chunk
+ * launch set: the default throughput form is one kernel (k_pairing_full) and the
+ * latency form one kernel (k_pairing_latency), both timed whole in ms[0] (ms[1..3] = 0);
+ * the three-launch forms ($BN254MI_MILLER_FORM 0-2) split it as ms[0] k_prepare or
+ * k_pairing_fused, ms[1] k_miller / k_miller_seg, ms[2] k_fq12_vm, ms[3] k_fe_out;
+ * the segmented latency path ms[0] k_prepare_wide, ms[1] k_miller_seg, ms[2] k_horner_wide.
  * *launches = launch sets measured */
 int bn_get_phase_times(bn_ctx* ctx, float ms[4], int* launches);
 

@@ -296,6 +296,53 @@ def g2_to_affine(q):
     return out, rcs
 
 
+def g1_add(a, b):  # mod.rs:294-334
+    return binary("orc_g1_add", a, b, 12, 12, 12)
+
+
+def g2_add(a, b):
+    return binary("orc_g2_add", a, b, 24, 24, 24)
+
+
+def g1_neg(a):  # mod.rs:336-350
+    return unary("orc_g1_neg", a, 12)[0]
+
+
+def g2_neg(a):
+    return unary("orc_g2_neg", a, 24)[0]
+
+
+def g1_sub(a, b):  # mod.rs:352-358: a + (-b)
+    return g1_add(a, g1_neg(b))
+
+
+def g2_sub(a, b):
+    return g2_add(a, g2_neg(b))
+
+
+def g1_normalize(a):
+    """Group::normalize (lib.rs:391-398): to_affine then to_jacobian; zero unchanged."""
+    a = _u64(a, 12)
+    aff, rcs = g1_to_affine(a)
+    out = a.copy()
+    one = canon_to_mont_array([1]).reshape(4)
+    for k, rc in enumerate(rcs):
+        if rc == 0:
+            out[k] = np.concatenate([aff[k], one])
+    return out
+
+
+def g2_normalize(a):
+    a = _u64(a, 24)
+    aff, rcs = g2_to_affine(a)
+    out = a.copy()
+    one = np.concatenate([canon_to_mont_array([1]).reshape(4), np.zeros(4, np.uint64)])
+    for k, rc in enumerate(rcs):
+        if rc == 0:
+            out[k] = np.concatenate([aff[k], one])
+    return out
+
+
 def g1_eq(a, b):
     a, b = _u64(a, 12), _u64(b, 12)
     return [bool(lib().orc_g1_eq(_p(a[k]), _p(b[k]))) for k in range(a.shape[0])]

@@ -471,7 +471,10 @@ int latency_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int
     RET_IF(product_wide(c, slot_region(c, kRegionSeg), n, n, n, 1, slot_region(c, kRegionResult), 1, 0, 1, s));
     return recombine_one(c, cut_plan(1, 1), do_fe, d_out, s);  // one segment: the FE of the product when do_fe
 }
-bool use_latency_product(const bn_ctx* c, size_t n) { return n <= c->latency_max && n <= c->fe_wide_max; }
+// (at most one chunk: the one-launch path reserves workspace for all n pairs)
+bool use_latency_product(const bn_ctx* c, size_t n) {
+    return n <= c->latency_max && n <= c->fe_wide_max && n <= kChunk;
+}
 
 // the whole product of n device pairs into *d_out; the caller holds the workspace
 int miller_product_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int mode, bn_gt* d_out,
@@ -490,11 +493,14 @@ int miller_product_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, 
     return finish_product(c, plan, nchunks, mode == 0, d_out, s);
 }
 
+// the device outcome bits of the calls since the last clear; a wave hand-off that
+// ran out of its wait cap (BN_ERR_INTERNAL) fails the call here, whatever else is set
 int check_err(bn_ctx* c, hipStream_t s, int* out_bits) {
     int h = 0;
     HIPCHK(c, hipMemcpyAsync(&h, c->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     *out_bits = h;
+    if (h & (1 << BN_ERR_INTERNAL)) return fail(c, BN_ERR_INTERNAL, "device wave hand-off timed out; result discarded");
     return BN_OK;
 }
 int clear_err(bn_ctx* c, hipStream_t s) {
@@ -764,7 +770,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             if (c->timing) c->ev_marks.push_back(ev);
             continue;
         }
-        if (c->miller_form == 1) {
+        if (c->miller_form == 1 || c->miller_form == 3) {  // form 3 without fe_last_out: the fused form
             k_pairing_fused<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(d_p + off, d_q + off, m, c->flags, c->d_err, 0,
                                                                         c->slots);
             mark(1);
@@ -796,6 +802,28 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
 int bn_pairing_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, bn_gt* d_out, void* stream) {
     CTX_GUARD(c);
     return pairing_many_dev_impl(c, d_p, d_q, n, d_out, pick(c, stream));
+}
+
+int bn_dev_status(bn_ctx* c, void* stream) {
+    if (c && !c->subs.empty()) {
+        int rc = BN_OK;
+        for (bn_ctx* d : c->subs) {
+            const int r = bn_dev_status(d, nullptr);
+            if (r != BN_OK && (rc == BN_OK || r == BN_ERR_INTERNAL)) rc = r;
+        }
+        return rc;
+    }
+    CTX_GUARD(c);
+    const hipStream_t s = pick(c, stream);
+    RET_IF(ws_acquire(c, s));  // after every workspace user, on any stream
+    WsUse use{c, s};
+    int bits = 0;
+    const int rc = check_err(c, s, &bits);
+    RET_IF(clear_err(c, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (rc) return rc;
+    if (bits & (1 << BN_ERR_FE_ZERO)) return fail(c, BN_ERR_FE_ZERO, "miller loop cannot produce zero");
+    return BN_OK;
 }
 
 int bn_set_phase_timing(bn_ctx* c, int enable) {
@@ -1345,6 +1373,109 @@ int bn_gt_pow_many(bn_ctx* c, const bn_gt* a, const bn_fr* k, size_t n, bn_gt* o
                                                                          c->slots);
                       return BN_OK;
                   });
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- group law
+// (lib.rs:388-423, 539-574; mod.rs:169-216, 294-358): one lane per element,
+// k_g1_op / k_g2_op.  Host forms stage chunks of kChunk elements through the
+// context; _dev forms enqueue on the stream.  b is read for add / sub / eq only.
+template <class P>
+static void group_launch(int op, const P* a, const P* b, size_t n, P* out, uint8_t* eq, hipStream_t s) {
+    if constexpr (sizeof(P) == sizeof(bn_g1))
+        k_g1_op<<<grid_for(n), kBlock, 0, s>>>(op, a, b, n, out, eq);
+    else
+        k_g2_op<<<grid_for(n), kBlock, 0, s>>>(op, a, b, n, out, eq);
+}
+static bool group_binary(int op) { return op == kGroupAdd || op == kGroupSub || op == kGroupEq; }
+template <class P>
+static int group_host(bn_ctx* c, int op, const P* a, const P* b, size_t n, P* out, uint8_t* eq) {
+    CTX_GUARD_HOST(c);
+    const bool two = group_binary(op);
+    auto run = [&](void** d, size_t m, hipStream_t s) -> int {
+        const P* db = two ? (const P*)d[1] : nullptr;
+        void* o = d[two ? 2 : 1];
+        group_launch<P>(op, (const P*)d[0], db, m, op == kGroupEq ? nullptr : (P*)o,
+                        op == kGroupEq ? (uint8_t*)o : nullptr, s);
+        return BN_OK;
+    };
+    const HostOut dst = op == kGroupEq ? HostOut{eq, 1} : HostOut{out, sizeof(P)};
+    if (two) return staged(c, n, {{a, sizeof(P)}, {b, sizeof(P)}}, {dst}, run);
+    return staged(c, n, {{a, sizeof(P)}}, {dst}, run);
+}
+template <class P>
+static int group_dev(bn_ctx* c, int op, const P* d_a, const P* d_b, size_t n, P* d_out, uint8_t* d_eq, void* stream) {
+    CTX_GUARD(c);
+    if (n == 0) return BN_OK;
+    if (!d_a || (group_binary(op) && !d_b) || (op == kGroupEq ? !d_eq : !d_out))
+        return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
+    group_launch<P>(op, d_a, group_binary(op) ? d_b : nullptr, n, d_out, d_eq, pick(c, stream));
+    HIPCHK(c, hipGetLastError());
+    return BN_OK;
+}
+
+extern "C" {
+
+int bn_g1_add_many(bn_ctx* c, const bn_g1* a, const bn_g1* b, size_t n, bn_g1* out) {
+    return group_host(c, kGroupAdd, a, b, n, out, nullptr);
+}
+int bn_g1_sub_many(bn_ctx* c, const bn_g1* a, const bn_g1* b, size_t n, bn_g1* out) {
+    return group_host(c, kGroupSub, a, b, n, out, nullptr);
+}
+int bn_g1_neg_many(bn_ctx* c, const bn_g1* a, size_t n, bn_g1* out) {
+    return group_host<bn_g1>(c, kGroupNeg, a, nullptr, n, out, nullptr);
+}
+int bn_g1_normalize_many(bn_ctx* c, const bn_g1* a, size_t n, bn_g1* out) {
+    return group_host<bn_g1>(c, kGroupNormalize, a, nullptr, n, out, nullptr);
+}
+int bn_g1_eq_many(bn_ctx* c, const bn_g1* a, const bn_g1* b, size_t n, uint8_t* eq) {
+    return group_host<bn_g1>(c, kGroupEq, a, b, n, nullptr, eq);
+}
+int bn_g2_add_many(bn_ctx* c, const bn_g2* a, const bn_g2* b, size_t n, bn_g2* out) {
+    return group_host(c, kGroupAdd, a, b, n, out, nullptr);
+}
+int bn_g2_sub_many(bn_ctx* c, const bn_g2* a, const bn_g2* b, size_t n, bn_g2* out) {
+    return group_host(c, kGroupSub, a, b, n, out, nullptr);
+}
+int bn_g2_neg_many(bn_ctx* c, const bn_g2* a, size_t n, bn_g2* out) {
+    return group_host<bn_g2>(c, kGroupNeg, a, nullptr, n, out, nullptr);
+}
+int bn_g2_normalize_many(bn_ctx* c, const bn_g2* a, size_t n, bn_g2* out) {
+    return group_host<bn_g2>(c, kGroupNormalize, a, nullptr, n, out, nullptr);
+}
+int bn_g2_eq_many(bn_ctx* c, const bn_g2* a, const bn_g2* b, size_t n, uint8_t* eq) {
+    return group_host<bn_g2>(c, kGroupEq, a, b, n, nullptr, eq);
+}
+int bn_g1_add_many_dev(bn_ctx* c, const bn_g1* d_a, const bn_g1* d_b, size_t n, bn_g1* d_out, void* stream) {
+    return group_dev(c, kGroupAdd, d_a, d_b, n, d_out, nullptr, stream);
+}
+int bn_g1_sub_many_dev(bn_ctx* c, const bn_g1* d_a, const bn_g1* d_b, size_t n, bn_g1* d_out, void* stream) {
+    return group_dev(c, kGroupSub, d_a, d_b, n, d_out, nullptr, stream);
+}
+int bn_g1_neg_many_dev(bn_ctx* c, const bn_g1* d_a, size_t n, bn_g1* d_out, void* stream) {
+    return group_dev<bn_g1>(c, kGroupNeg, d_a, nullptr, n, d_out, nullptr, stream);
+}
+int bn_g1_normalize_many_dev(bn_ctx* c, const bn_g1* d_a, size_t n, bn_g1* d_out, void* stream) {
+    return group_dev<bn_g1>(c, kGroupNormalize, d_a, nullptr, n, d_out, nullptr, stream);
+}
+int bn_g1_eq_many_dev(bn_ctx* c, const bn_g1* d_a, const bn_g1* d_b, size_t n, uint8_t* d_eq, void* stream) {
+    return group_dev<bn_g1>(c, kGroupEq, d_a, d_b, n, nullptr, d_eq, stream);
+}
+int bn_g2_add_many_dev(bn_ctx* c, const bn_g2* d_a, const bn_g2* d_b, size_t n, bn_g2* d_out, void* stream) {
+    return group_dev(c, kGroupAdd, d_a, d_b, n, d_out, nullptr, stream);
+}
+int bn_g2_sub_many_dev(bn_ctx* c, const bn_g2* d_a, const bn_g2* d_b, size_t n, bn_g2* d_out, void* stream) {
+    return group_dev(c, kGroupSub, d_a, d_b, n, d_out, nullptr, stream);
+}
+int bn_g2_neg_many_dev(bn_ctx* c, const bn_g2* d_a, size_t n, bn_g2* d_out, void* stream) {
+    return group_dev<bn_g2>(c, kGroupNeg, d_a, nullptr, n, d_out, nullptr, stream);
+}
+int bn_g2_normalize_many_dev(bn_ctx* c, const bn_g2* d_a, size_t n, bn_g2* d_out, void* stream) {
+    return group_dev<bn_g2>(c, kGroupNormalize, d_a, nullptr, n, d_out, nullptr, stream);
+}
+int bn_g2_eq_many_dev(bn_ctx* c, const bn_g2* d_a, const bn_g2* d_b, size_t n, uint8_t* d_eq, void* stream) {
+    return group_dev<bn_g2>(c, kGroupEq, d_a, d_b, n, nullptr, d_eq, stream);
 }
 
 }  // extern "C"

@@ -164,11 +164,11 @@ BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o) {
     return jac_add(s, o, jac_is_zero(o));
 }
 
-// mod.rs:336-350
+// mod.rs:336-350 (zero unchanged, else (x, -y, z)), at the storage bound
 template <template <int> class F>
 BN_INLINE Jac<F> jac_neg(const Jac<F>& a) {
     const bool z = jac_is_zero(a);
-    return {a.x, F_select(z, a.y, F_neg(a.y)), a.z};
+    return {a.x, F_select(z, a.y, narrow<kPt>(F_neg(a.y))), a.z};
 }
 
 // MSB-first double-and-add over the bits of the canonical scalar
@@ -176,19 +176,16 @@ BN_INLINE Jac<F> jac_neg(const Jac<F>& a) {
 // addition of p when the bit is set.  Every lane follows exactly the
 // reference's chain, so the Jacobian output is bit-identical.
 //
-// The chains differ per lane, so a wave schedules them (BN_MUL_SCHED = 1): each
+// The chains differ per lane, so a wave schedules them: each
 // iteration runs ONE kind of step -- the addition for the lanes whose next step
 // is an addition, or the doubling for those whose next step is a doubling --
 // chosen by a ballot: the addition once at least 3/5 of the unfinished lanes
 // wait for it (or no lane waits for a doubling).  A lane's own steps keep their
 // order, so its result is unchanged; lanes simply drift apart within the wave.
-// Lockstep execution (BN_MUL_SCHED = 0: every bit runs the doubling and the
-// masked addition on every lane) executes 253 x (7 + 16) Fq-mul per lane for
+// Lockstep execution (every bit runs the doubling and the masked addition on
+// every lane, round 2) executes 253 x (7 + 16) Fq-mul per lane for
 // random scalars; the scheduled chain ~8 % less (a simulation of 64 random
 // 254-bit scalars: 5,302 against 5,819 Fq-mul-weighted steps).
-#ifndef BN_MUL_SCHED
-#define BN_MUL_SCHED 1
-#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 #define BN_BALLOT_COUNT(p) ((uint32_t)__popcll(__ballot((int)(p))))
 #else
@@ -202,7 +199,6 @@ template <template <int> class F, typename Step = NoBitStep>
 BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8], Step&& step = Step{}) {
     Jac<F> res = jac_zero<F>();
     const bool p_zero = jac_is_zero(p);
-#if BN_MUL_SCHED
     // lane state: `w` holds the scalar shifted so that the next bit to consume is
     // bit 31 of w[7]; `left` = bits still to consume after the top set bit;
     // `need_add`: the lane's next step is the addition of the current bit
@@ -258,29 +254,6 @@ BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8], Step&& step = Ste
             w[0] = need_dbl ? w[0] << 1 : w[0];
         }
     }
-#else
-    bool found_one = false;
-    uint32_t w[8];  // scalar, shifted left one bit per step (no indexed private arrays)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = k[i];
-#pragma unroll 1
-    for (int bit = 255; bit >= 0; --bit) {
-        step(255 - bit);
-        const bool b = w[7] >> 31;
-#pragma unroll
-        for (int i = 7; i > 0; --i) w[i] = (w[i] << 1) | (w[i - 1] >> 31);
-        w[0] <<= 1;
-        if (BN_ANY(found_one)) {
-            Jac<F> d = jac_double(res);
-            res = {F_select(found_one, d.x, res.x), F_select(found_one, d.y, res.y), F_select(found_one, d.z, res.z)};
-        }
-        if (BN_ANY(b)) {
-            Jac<F> a = jac_add(res, p, p_zero);
-            res = {F_select(b, a.x, res.x), F_select(b, a.y, res.y), F_select(b, a.z, res.z)};
-            found_one = found_one || b;
-        }
-    }
-#endif
     return res;
 }
 

@@ -6,9 +6,6 @@
 
 namespace bn {
 
-#ifndef BN_VM_PRELOAD
-#define BN_VM_PRELOAD 0
-#endif
 __device__ __forceinline__ uint32_t* vm_slot_ptr(uint32_t* slots, size_t nl, uint32_t s) {
     return slots + (size_t)s * kSlotLaneWords * nl;
 }
@@ -42,20 +39,15 @@ __device__ __forceinline__ Fq12<kF> fq12_vm_run(const uint32_t* __restrict__ pro
         switch (op) {
             case OP_MOV: r = x; break;
             case OP_MUL: {
-#if BN_VM_PRELOAD
-                // the operand's loads issued before the squarings (A/B: their
-                // latency hidden, 54 more live VGPRs across the squarings)
-                Fq12<kF> y = ld_fq12_buf<kF>(b, nn, i);
-#endif
+                // (the operand loaded before the squarings instead: more scratch, within
+                // noise, profiles/r3v_ab_vm_preload.txt)
 #pragma unroll 1
                 for (uint32_t j = 0; j < k; ++j) {
                     balance_step(bal, pos | j);
                     x = cyc_sqr(x);
                 }
                 balance_step(bal, pos | 255u);
-#if !BN_VM_PRELOAD
                 Fq12<kF> y = ld_fq12_buf<kF>(b, nn, i);
-#endif
                 if (flags & kFlagConjB) y = fq12_conj(y);
                 r = mul12(x, y);
                 if (flags & kFlagConjOut) r = fq12_conj(r);

@@ -37,9 +37,6 @@
 #define BN_INLINE inline __attribute__((always_inline))
 #endif
 
-#ifndef BN_FENCE_FQ
-#define BN_FENCE_FQ 0
-#endif
 // Layout of the pairing-path kernels: 1 = two lanes per element (fq2_split.h),
 // 0 = one lane per element.  A pairing-path translation unit sets
 // BN_SPLIT = BN_PATH_SPLIT before including kernels.h; every other unit
@@ -275,15 +272,8 @@ BN_INLINE auto fq_mul(const Fq<A>& a_in, const Fq<B>& b_in) {
         if constexpr (kl(A) >= kl(B)) return fq_mul(fq_norm(a_in), b_in); else return fq_mul(a_in, fq_norm(b_in));
     } else {
     static_assert((long long)kv(A) * kv(B) <= 160 * 160, "product bound");
-#if BN_FENCE_FQ
-    Fq<A> a = a_in;
-    Fq<B> b = b_in;
-    fq_fence(a);
-    fq_fence(b);
-#else
     const Fq<A>& a = a_in;
     const Fq<B>& b = b_in;
-#endif
     uint32_t m[9];
     Fq<mul_bound(kv(A), kv(B))> r;
     uint64_t acc = 0;
@@ -305,9 +295,6 @@ BN_INLINE auto fq_mul(const Fq<A>& a_in, const Fq<B>& b_in) {
         acc >>= 29;
     }
     r.v[8] = (uint32_t)acc;
-#if BN_FENCE_FQ
-    fq_fence(r);
-#endif
     return r;
     }
 }
@@ -315,12 +302,8 @@ BN_INLINE auto fq_mul(const Fq<A>& a_in, const Fq<B>& b_in) {
 // (i < j) taken once against the doubled digit 2*a_j, so a column holds at most
 // four cross products (< 2L^2 * 2^58 each), one square and nine m*p terms:
 // 45 + 81 digit products instead of 81 + 81.  The same residue as fq_mul(a, a).
-#ifndef BN_FQ_SQR
-#define BN_FQ_SQR 1
-#endif
 template <int B>
 BN_INLINE auto fq_sqr(const Fq<B>& a_in) {
-#if BN_FQ_SQR
     if constexpr (kl(B) > 2) {
         return fq_sqr(fq_norm(a_in));
     } else {
@@ -355,9 +338,6 @@ BN_INLINE auto fq_sqr(const Fq<B>& a_in) {
     r.v[8] = (uint32_t)acc;
     return r;
     }
-#else
-    return fq_mul(a_in, a_in);
-#endif
 }
 
 // bring any value back to bound 2 (a Montgomery product with one)

@@ -139,9 +139,7 @@ constexpr uint64_t kWSqrTerm[4] = {
     w_sqr_term(w_sqr_code(2, 0, 0), w_sqr_code(1, 3, 4), w_sqr_code(2, 1, 1), w_sqr_code(1, 4, 5), w_sqr_code(2, 2, 2), w_sqr_code(0, 2, 3)),
     w_sqr_term(w_sqr_code(3, 3, 3), w_sqr_code(3, 6, 0), w_sqr_code(3, 4, 4), w_sqr_code(3, 6, 0), w_sqr_code(3, 5, 5), w_sqr_code(3, 6, 0)),
 };
-#ifndef BN_WIDE_SQR
-#define BN_WIDE_SQR 1  // 0: squares by w12_mul(a, a) (A/B)
-#endif
+// (squarings as w12_mul(a, a) instead: within 1 %, profiles/r3y_ab_wide_sqr.txt)
 __device__ __noinline__ Fq<2> w12_sqr(Fq<2> a) {
     const WL w = wl();
     uint32_t* A_ = w.gb;
@@ -457,8 +455,13 @@ constexpr int kDuoRing = 4;                       // S -> M items in flight
 constexpr int kDuoWords = (kDuoRing + 2) * kWArr;  // channel words per element
 constexpr uint32_t kDuoSpinCap = 1u << 26;        // ~4 s of s_sleep 1: never reached while both run
 
-__device__ __forceinline__ void duo_wait(const volatile uint32_t* c, uint32_t v) {
-    for (uint32_t spins = 0; *c < v && spins < kDuoSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
+// A wait that runs out of its cap would go on to read a slot that was never
+// published: it sets the BN_ERR_INTERNAL bit of *err, so the call fails
+// (check_err, bn_dev_status) instead of returning a wrong Gt.
+__device__ __forceinline__ void duo_wait(const volatile uint32_t* c, uint32_t v, int* err) {
+    uint32_t spins = 0;
+    for (; *c < v && spins < kDuoSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
+    if (spins == kDuoSpinCap && err) atomicOr(err, 1 << BN_ERR_INTERNAL);
     asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void duo_signal(volatile uint32_t* c, uint32_t v) {
@@ -469,13 +472,14 @@ struct WDuo {
     uint32_t* ch;           // kDuoWords words of LDS
     volatile uint32_t* cnt;  // three counters, zero at the start
     uint32_t items, results;
+    int* err;  // device error word: BN_ERR_INTERNAL when a wait runs out of its cap
     __device__ void put(const Fq<2>& x) {  // S
-        if (items >= (uint32_t)kDuoRing) duo_wait(cnt + 1, items + 1 - kDuoRing);
+        if (items >= (uint32_t)kDuoRing) duo_wait(cnt + 1, items + 1 - kDuoRing, err);
         w_put(ch + (items % kDuoRing) * kWArr, (int)(threadIdx.x & (kWLanes - 1)), x);
         duo_signal(cnt, ++items);
     }
     __device__ Fq<2> take() {  // M
-        duo_wait(cnt, items + 1);
+        duo_wait(cnt, items + 1, err);
         const Fq<2> x = w_get<2>(ch + (items % kDuoRing) * kWArr, (int)(threadIdx.x & (kWLanes - 1)));
         duo_signal(cnt + 1, ++items);
         return x;
@@ -485,7 +489,7 @@ struct WDuo {
         duo_signal(cnt + 2, ++results);
     }
     __device__ Fq<2> get_result() {  // S
-        duo_wait(cnt + 2, results + 1);
+        duo_wait(cnt + 2, results + 1, err);
         const Fq<2> x = w_get<2>(ch + (kDuoRing + results % 2) * kWArr, (int)(threadIdx.x & (kWLanes - 1)));
         ++results;
         return x;

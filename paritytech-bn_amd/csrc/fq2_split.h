@@ -117,21 +117,9 @@ BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) {
     const uint32_t e = fq_eq(a.c, b.c) ? 1u : 0u;
     return (e & swap_pair(e)) != 0;
 }
-#ifndef BN_FQ2_FENCE
-#define BN_FQ2_FENCE 1
-#endif
-// 1: the split Fq2 product takes its operand's c0 / c1 on both lanes by DPP
-// broadcast (quad_perm) instead of a partner swap plus a per-lane select
-#ifndef BN_FQ2_BCAST
-#define BN_FQ2_BCAST 1
-#endif
 template <int B>
 BN_INLINE void fq2_fence(Fq2<B>& a) {
-#if BN_FQ2_FENCE
     fq_fence(a.c);
-#else
-    (void)a;
-#endif
 }
 
 // K*p - x without a carry pass (digits < (sub_spread(L)+2)*2^29, value <= (B+1)*p)
@@ -143,21 +131,13 @@ BN_INLINE Fq<kenc(kv(K) + 1, sub_spread(kl(K)) + 2)> fq_neg_lazy(const Fq<K>& x)
     for (int i = 0; i < 9; ++i) r.v[i] = Q.v[i] - x.v[i];
     return r;
 }
-// 1: fq2_mul_split takes its w operand (lane 0: K*p - b1, lane 1: b1) as one
+// fq2_mul_split takes its w operand (lane 0: K*p - b1, lane 1: b1) as one
 // v_cndmask_b32_dpp per digit -- odd lanes keep their own b1, even lanes take the
 // partner's K*p - b1 through the DPP swap -- instead of a broadcast, a negation
 // and a select: 9 VALU fewer per product, k_pairing_full 7.79-7.81 -> 7.73-7.75 ms
-// (profiles/r3r_ab_dppsel.txt; 2: VCC written by a VALU compare, 7.75-7.76 ms;
-// 0: the broadcast form)
-#ifndef BN_FQ2_DPPSEL
-#define BN_FQ2_DPPSEL 1
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_DPPSEL
-#if BN_FQ2_DPPSEL == 2
-#define BN_DPPSEL_VCC "v_cmp_ne_u32_e32 vcc, 0, %27\n\ts_nop 1\n\t"
-#else
+// (profiles/r3r_ab_dppsel.txt)
+#if defined(__HIP_DEVICE_COMPILE__)
 #define BN_DPPSEL_VCC "s_mov_b32 vcc_lo, 0xaaaaaaaa\n\ts_mov_b32 vcc_hi, 0xaaaaaaaa\n\ts_nop 1\n\t"
-#endif
 #define BN_DPPSEL_OP(o, a, b) "v_cndmask_b32_dpp %" #o ", %" #a ", %" #b ", vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
 // w[i] = odd lane ? own[i] : the partner's neg[i].  The s_nop covers the two
 // wait states a DPP read needs after the VALU write of its source (the hazard
@@ -173,26 +153,6 @@ BN_INLINE void dpp_sel_own_partner(uint32_t (&w)[9], const uint32_t (&own)[9], c
           "v"(neg[8]), "v"(own[0]), "v"(own[1]), "v"(own[2]), "v"(own[3]), "v"(own[4]), "v"(own[5]), "v"(own[6]),
           "v"(own[7]), "v"(own[8]), "v"(odd)
         : "vcc");
-}
-#endif
-// 1: x * xi adds the partner's term with one v_add_u32_dpp per digit instead of
-// a DPP move and an add (A/B: no gain, 7.79-7.81 ms, and slower on top of
-// BN_FQ2_DPPSEL, profiles/r3r_ab_dppsel.txt)
-#ifndef BN_XI_DPPADD
-#define BN_XI_DPPADD 0
-#endif
-#if defined(__HIP_DEVICE_COMPILE__) && BN_XI_DPPADD
-#define BN_DPPADD_OP(o, a, b) "v_add_u32_dpp %" #o ", %" #a ", %" #b " quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-// r[i] = own[i] + the partner's s[i] (s_nop: the DPP source's VALU-write hazard)
-BN_INLINE void dpp_add_partner(uint32_t (&r)[9], const uint32_t (&own)[9], const uint32_t (&s)[9]) {
-    asm("s_nop 1\n\t" BN_DPPADD_OP(0, 9, 18) BN_DPPADD_OP(1, 10, 19) BN_DPPADD_OP(2, 11, 20) BN_DPPADD_OP(3, 12, 21)
-            BN_DPPADD_OP(4, 13, 22) BN_DPPADD_OP(5, 14, 23) BN_DPPADD_OP(6, 15, 24) BN_DPPADD_OP(7, 16, 25)
-                BN_DPPADD_OP(8, 17, 26)
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
-          "=&v"(r[8])
-        : "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]), "v"(s[6]), "v"(s[7]), "v"(s[8]),
-          "v"(own[0]), "v"(own[1]), "v"(own[2]), "v"(own[3]), "v"(own[4]), "v"(own[5]), "v"(own[6]), "v"(own[7]),
-          "v"(own[8]));
 }
 #endif
 // per-lane choice between two values of different static types (the join)
@@ -255,17 +215,12 @@ BN_INLINE auto fq2_mul_split(const Fq2<A>& a, const Fq2<B>& b) {
     } else {
         const bool odd = lane_odd();
         const Fq<A> pa = fq_partner(a.c);
-#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_DPPSEL
+#if defined(__HIP_DEVICE_COMPILE__)
         const Fq<B> y = fq_bcast_c0(b.c);
         const auto nb = fq_neg_lazy(b.c);  // the odd lane's is K*p - b1
         Fq<kjoin(B, kenc(kv(B) + 1, sub_spread(kl(B)) + 2))> w;
         dpp_sel_own_partner(w.v, b.c.v, nb.v);
         (void)odd;
-#elif defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_BCAST
-        // y = b0 and c1 = b1 on both lanes straight from DPP (no select for y)
-        const Fq<B> y = fq_bcast_c0(b.c);
-        const Fq<B> c1 = fq_bcast_c1(b.c);
-        const auto w = fq_pick(odd, c1, fq_neg_lazy(c1));
 #else
         const Fq<B> pb = fq_partner(b.c);
         const Fq<B> y = fq_select(odd, pb, b.c);
@@ -338,16 +293,8 @@ BN_INLINE auto fq2_mul_xi(const Fq2<A>& a) {
     } else {
         const Fq<kv(A)> own = fq_norm(a.c);
         const auto own9 = fq_add(fq_mul_small<8>(own), own);
-#if defined(__HIP_DEVICE_COMPILE__) && BN_XI_DPPADD
-        // the odd lane offers K*p - a1 to its partner, the even lane a0
-        const auto s = fq_pick(lane_odd(), fq_neg_lazy(own), own);
-        decltype(fq_add(own9, s)) r;
-        dpp_add_partner(r.v, own9.v, s.v);
-        return wrap2(r);
-#else
         const Fq<kv(A)> par = fq_partner(own);
         return wrap2(fq_add(own9, fq_pick(lane_odd(), par, fq_neg_lazy(par))));
-#endif
     }
 }
 // fq2.rs:59-68: odd powers conjugate: lane 1 negates (c1 * (p-1) == -c1)

@@ -20,11 +20,9 @@ constexpr int kPathLanes = BN_PATH_SPLIT ? 2 : 1;
 // words of one Fq12 slot per lane of the translation unit's own layout
 constexpr int kSlotLaneWords = BN_SPLIT ? 54 : 108;
 #if BN_SPLIT
-// two waves per SIMD: the kernel must fit 256 registers (BN_PATH_WAVES: A/B builds)
-#ifndef BN_PATH_WAVES
-#define BN_PATH_WAVES 2
-#endif
-#define BN_PATH_ATTR __attribute__((amdgpu_waves_per_eu(BN_PATH_WAVES, BN_PATH_WAVES)))
+// two waves per SIMD: the kernel must fit 256 registers (three or four waves: the
+// spills cost 20-40 %, profiles/r2u_ab_waves_per_simd.txt)
+#define BN_PATH_ATTR __attribute__((amdgpu_waves_per_eu(2, 2)))
 #else
 #define BN_PATH_ATTR
 #endif
@@ -397,22 +395,15 @@ __device__ __forceinline__ size_t lane_id() { return (size_t)blockIdx.x * blockD
 // its priority (s_setprio) to the number of waves on its SIMD (found from
 // HW_ID's SIMD field at start) that are AHEAD of it, so laggards issue first and
 // the waves finish together.  Scheduling only: no value depends on it.
-// BN_BALANCE=0 builds the plain form (A/B): 7.6 -> 8.3 M pairings/s
-// (profiles/r3a_ab_balance.txt).
-#ifndef BN_BALANCE
-#define BN_BALANCE 1
-#endif
-#ifndef BN_PAIR_BLOCK
-#define BN_PAIR_BLOCK 512
-#endif
-constexpr int kPairBlock = BN_PAIR_BLOCK;
+// Without it: 7.6 instead of 8.3 M pairings/s (profiles/r3a_ab_balance.txt).
+constexpr int kPairBlock = 512;
 constexpr int kMaxBlock = 1024;
 struct Balance {
     uint32_t w = 0;        // this wave's index in the block
     uint32_t partner = 0;  // the first other wave of the block on this wave's SIMD (itself if none)
     uint32_t more = 0;     // any further ones (bit j = wave j): more than two waves per SIMD
 };
-#if BN_BALANCE && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
 __shared__ uint32_t g_bal_prog[kMaxBlock / 64];
 __shared__ uint32_t g_bal_simd[kMaxBlock / 64];
 // every thread of the block calls this (it has a barrier), before any early return
@@ -577,6 +568,12 @@ __global__ void __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g,
 __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict__ f, size_t n, size_t stride, bn_gt* __restrict__ g);
 __global__ void __launch_bounds__(kPairBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g1* __restrict__ out);
 __global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g2* __restrict__ out);
+// the group law (kernels_group.hip): op codes of k_g1_op / k_g2_op (b may be null for neg / normalize)
+enum GroupOp { kGroupAdd = 0, kGroupSub = 1, kGroupNeg = 2, kGroupNormalize = 3, kGroupEq = 4 };
+__global__ void __launch_bounds__(kBlock) k_g1_op(int op, const bn_g1* __restrict__ a, const bn_g1* __restrict__ b,
+                                                  size_t n, bn_g1* __restrict__ out, uint8_t* __restrict__ eq);
+__global__ void __launch_bounds__(kBlock) k_g2_op(int op, const bn_g2* __restrict__ a, const bn_g2* __restrict__ b,
+                                                  size_t n, bn_g2* __restrict__ out, uint8_t* __restrict__ eq);
 __global__ void __launch_bounds__(kPairBlock) k_gt_pow(const bn_gt* __restrict__ a, const bn_fr* __restrict__ k, size_t n,
                                                    bn_gt* __restrict__ out, uint32_t* __restrict__ ws);
 // kernels_codec.hip (codec.h): encodings, square roots, validation, decompression

@@ -1,4 +1,5 @@
-// kernels_group.hip -- batched G1/G2 scalar multiplication (mod.rs:272-292), one lane per product.
+// kernels_group.hip -- batched G1/G2 scalar multiplication (mod.rs:272-292) and
+// the group law (mod.rs:169-216, 294-358), one lane per element.
 // fq_fold reads -q*p from an LDS table (fq.h; every kernel here calls
 // fold_table_init first)
 #ifndef BN_FOLD_LDS
@@ -36,6 +37,79 @@ __global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, 
     fr_to_canonical(k[i], s);
     G2J a = {widen<kPt>(ld_ref2(p[i].x)), widen<kPt>(ld_ref2(p[i].y)), widen<kPt>(ld_ref2(p[i].z))};
     G2J r = jac_mul(a, s);
+    st_ref2(out[i].x, r.x);
+    st_ref2(out[i].y, r.y);
+    st_ref2(out[i].z, r.z);
+}
+
+// ---------------------------------------------------------------- group law
+// Group::normalize (lib.rs:391-398, 542-549): to_affine (mod.rs:199-216), then
+// to_jacobian (mod.rs:220-226: z = one); a zero point stays as it is.  The
+// inverse is unique, so (x z^-2, y z^-3, 1) is the reference's image also when z
+// is already one (its shortcut returns the same residues).
+template <template <int> class F>
+__device__ __forceinline__ Jac<F> jac_normalize(const Jac<F>& a) {
+    const bool zero = jac_is_zero(a);
+    const auto zinv = F_inv(a.z);  // F_inv(0) = 0; that result is discarded
+    const auto zinv2 = F_sqr(zinv);
+    const Jac<F> r = {narrow<kPt>(F_mul(a.x, zinv2)), narrow<kPt>(F_mul(a.y, F_mul(zinv2, zinv))),
+                      F_widen<kPt>(F_one<F>())};
+    return {F_select(zero, a.x, r.x), F_select(zero, a.y, r.y), F_select(zero, a.z, r.z)};
+}
+// PartialEq for G<P> (mod.rs:169-195): both zero, or neither and
+// x1 z2^2 == x2 z1^2 and y1 z2^3 == y2 z1^3 (mod p)
+template <template <int> class F>
+__device__ __forceinline__ bool jac_eq(const Jac<F>& a, const Jac<F>& b) {
+    const bool az = jac_is_zero(a), bz = jac_is_zero(b);
+    const auto z1sq = F_sqr(a.z);
+    const auto z2sq = F_sqr(b.z);
+    const bool ex = F_is_zero(F_sub(F_mul(a.x, z2sq), F_mul(b.x, z1sq)));
+    const auto z1cu = F_mul(a.z, z1sq);
+    const auto z2cu = F_mul(b.z, z2sq);
+    const bool ey = F_is_zero(F_sub(F_mul(a.y, z2cu), F_mul(b.y, z1cu)));
+    return az ? bz : (!bz && ex && ey);
+}
+// out[i] = a[i] op b[i] (op: GroupOp, kernels.h; wave-uniform); kGroupEq writes
+// eq[i] instead of out[i]
+template <template <int> class F>
+__device__ __forceinline__ Jac<F> group_apply(int op, const Jac<F>& x, const Jac<F>& y) {
+    switch (op) {
+        case kGroupAdd: return jac_add(x, y);                // mod.rs:294-334
+        case kGroupSub: return jac_add(x, jac_neg(y));     // mod.rs:352-358: self + (-other)
+        case kGroupNeg: return jac_neg(x);                 // mod.rs:336-350
+        default: return jac_normalize(x);                     // kGroupNormalize
+    }
+}
+__global__ void __launch_bounds__(kBlock) k_g1_op(int op, const bn_g1* __restrict__ a, const bn_g1* __restrict__ b,
+                                                  size_t n, bn_g1* __restrict__ out, uint8_t* __restrict__ eq) {
+    fold_table_init();
+    const size_t i = lane_id();
+    if (i >= n) return;
+    const G1J x = {widen<kPt>(ld_ref(a[i].x)), widen<kPt>(ld_ref(a[i].y)), widen<kPt>(ld_ref(a[i].z))};
+    G1J y = x;
+    if (b) y = {widen<kPt>(ld_ref(b[i].x)), widen<kPt>(ld_ref(b[i].y)), widen<kPt>(ld_ref(b[i].z))};
+    if (op == kGroupEq) {
+        eq[i] = jac_eq(x, y) ? 1 : 0;
+        return;
+    }
+    const G1J r = group_apply(op, x, y);
+    st_ref(out[i].x, r.x);
+    st_ref(out[i].y, r.y);
+    st_ref(out[i].z, r.z);
+}
+__global__ void __launch_bounds__(kBlock) k_g2_op(int op, const bn_g2* __restrict__ a, const bn_g2* __restrict__ b,
+                                                  size_t n, bn_g2* __restrict__ out, uint8_t* __restrict__ eq) {
+    fold_table_init();
+    const size_t i = lane_id();
+    if (i >= n) return;
+    const G2J x = {widen<kPt>(ld_ref2(a[i].x)), widen<kPt>(ld_ref2(a[i].y)), widen<kPt>(ld_ref2(a[i].z))};
+    G2J y = x;
+    if (b) y = {widen<kPt>(ld_ref2(b[i].x)), widen<kPt>(ld_ref2(b[i].y)), widen<kPt>(ld_ref2(b[i].z))};
+    if (op == kGroupEq) {
+        eq[i] = jac_eq(x, y) ? 1 : 0;
+        return;
+    }
+    const G2J r = group_apply(op, x, y);
     st_ref2(out[i].x, r.x);
     st_ref2(out[i].y, r.y);
     st_ref2(out[i].z, r.z);

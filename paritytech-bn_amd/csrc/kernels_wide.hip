@@ -7,11 +7,6 @@
 #ifndef BN_FOLD_LDS
 #define BN_FOLD_LDS 1
 #endif
-// 1: idle groups of a block (past n) run on a copy of the last element instead
-// of returning (A/B: the cost of a wave with a single active group)
-#ifndef BN_WIDE_PAD
-#define BN_WIDE_PAD 1
-#endif
 #include "fq.h"
 #define BN_SPLIT 1
 #include "fq12_wide.h"
@@ -63,39 +58,42 @@ __device__ __forceinline__ void w_duo_init() {
 }
 // the final exponentiation on S (with its M running w12_final_exp_m), or on
 // the group alone
-__device__ __forceinline__ Fq<2> w_final_exp(const WRole& r, const Fq<2>& x) {
+__device__ __forceinline__ Fq<2> w_final_exp(const WRole& r, const Fq<2>& x, int* err) {
 #if BN_FE_DUO
     if (r.duo) {
-        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0};
+        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0, err};
         return w12_final_exp_s(x, d);
     }
 #endif
     (void)r;
+    (void)err;
     return w12_final_exp(x);
 }
 // the last chunk only, of s = w12_fe_first(x) (k_horner_tree)
-__device__ __forceinline__ Fq<2> w_fe_last(const WRole& r, const Fq<2>& s) {
+__device__ __forceinline__ Fq<2> w_fe_last(const WRole& r, const Fq<2>& s, int* err) {
 #if BN_FE_DUO
     if (r.duo) {
-        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0};
+        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0, err};
         return w12_fe_last_s(s, d);
     }
 #endif
     (void)r;
+    (void)err;
     return w12_fe_last(s);
 }
 // M's part; true if this group is M (and has done it)
-__device__ __forceinline__ bool w_final_exp_m(const WRole& r, bool run) {
+__device__ __forceinline__ bool w_final_exp_m(const WRole& r, bool run, int* err) {
 #if BN_FE_DUO
     if (r.sq) return false;
     if (run) {
-        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0};
+        WDuo d = {g_wduo_ch + r.slot * kDuoWords, g_wduo_cnt + 4 * r.slot, 0, 0, err};
         w12_final_exp_m(d);
     }
     return true;
 #else
     (void)r;
     (void)run;
+    (void)err;
     return false;
 #endif
 }
@@ -110,21 +108,17 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
     fold_table_init();
     w_duo_init();
     const WRole role = w_role(duo != 0);
-#if BN_WIDE_PAD
+    // idle groups of the block (past n) repeat the last element instead of returning:
+    // a wave whose other groups had returned ran its last group ~200 us slower
     const bool live = role.e < n;
-    const size_t e = live ? role.e : n - 1;  // idle groups of the block repeat the last element
-#else
-    const bool live = true;
-    const size_t e = role.e;
-    if (e >= n) return;
-#endif
-    if (w_final_exp_m(role, true)) return;
+    const size_t e = live ? role.e : n - 1;
+    if (w_final_exp_m(role, true, err)) return;
     const WL w = wl();
     const Fq<2> x = w_ld_split(f, stride, e, w);
     const bool zero = w12_is_zero(x);
     if (ok && w.l == 0 && live) ok[e] = zero ? 0 : 1;
     if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
-    const Fq<2> r = w_final_exp(role, x);
+    const Fq<2> r = w_final_exp(role, x, err);
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!zero) fq_store_ref(r, words);
     if (w.l < 12 && live) st_words(&out[e].c[w_gt_index(w)], words);
@@ -194,15 +188,11 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
     fold_table_init();
     w_duo_init();
     const WRole role = w_role(duo != 0);
-#if BN_WIDE_PAD
+    // idle groups of the block (past n) repeat the last element instead of returning:
+    // a wave whose other groups had returned ran its last group ~200 us slower
     const bool live = role.e < n;
-    const size_t e = live ? role.e : n - 1;  // idle groups of the block repeat the last element
-#else
-    const bool live = true;
-    const size_t e = role.e;
-    if (e >= n) return;
-#endif
-    if (w_final_exp_m(role, do_fe != 0)) return;
+    const size_t e = live ? role.e : n - 1;
+    if (w_final_exp_m(role, do_fe != 0, err)) return;
     const WL w = wl();
     const size_t stride = (size_t)plan.S * n;
     Fq<2> x = w_ld_split(g, stride, e, w);
@@ -210,7 +200,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
 #pragma unroll 1
     for (int s = 1; s < plan.S; ++s) {
 #pragma unroll 1
-        for (int k = plan.lo[s]; k < plan.hi[s]; ++k) x = BN_WIDE_SQR ? w12_sqr(x) : w12_mul(x, x);
+        for (int k = plan.lo[s]; k < plan.hi[s]; ++k) x = w12_sqr(x);
         if (s == 1) HOR_STAMP(2);  // the first run of squarings
         x = w12_mul(x, w_ld_split(g, stride, (size_t)s * n + e, w));
         if (s == 1) HOR_STAMP(3);  // its load + product
@@ -220,7 +210,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
     if (do_fe) {
         const bool zero = w12_is_zero(x);
         if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
-        const Fq<2> r = w_final_exp(role, x);
+        const Fq<2> r = w_final_exp(role, x, err);
         HOR_STAMP(5);  // final exponentiation done
         if (!zero) fq_store_ref(r, words);
     } else {
@@ -258,6 +248,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restri
                                                         bn_gt* __restrict__ out, int* __restrict__ err, int duo) {
     HOR_STAMP(0);  // start
     if (threadIdx.x == 0) g_hor_zero = 0;
+    __syncthreads();  // the reset is seen before any group can set the flag
     fold_table_init();
     w_duo_init();
     const WL w = wl();
@@ -283,7 +274,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restri
     } else {
 #pragma unroll 1
         for (int k = 0; k < e0; ++k) {
-            const Fq<2> y = BN_WIDE_SQR ? w12_sqr(x) : w12_mul(x, x);
+            const Fq<2> y = w12_sqr(x);
             x = k < e ? y : x;
         }
     }
@@ -303,12 +294,12 @@ __global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restri
     x = w_get<2>(g_wval, w.l);
     HOR_STAMP(4);  // recombination done
     const WRole role = w_role(duo != 0);  // group g < 8: S of channel g; group g + 8: its M
-    if (w_final_exp_m(role, do_fe != 0)) return;
+    if (w_final_exp_m(role, do_fe != 0, err)) return;
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (do_fe) {
         const bool zero = g_hor_zero != 0;
         if (zero && err && w.l == 0 && grp == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
-        const Fq<2> r = w_fe_last(role, x);
+        const Fq<2> r = w_fe_last(role, x, err);
         HOR_STAMP(5);  // final exponentiation done
         if (!zero) fq_store_ref(r, words);
     } else {
@@ -338,7 +329,8 @@ __global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restri
 // its LDS writes (lgkmcnt(0)) and bumps the pair's `prod` counter; a consumer
 // spins (s_sleep) until `prod` passes the line it needs and bumps `cons` after
 // reading it; the producer keeps at most kLatRing lines ahead.  Both sides
-// always progress, so every wave reaches the end; the spins are capped anyway.
+// always progress, so every wave reaches the end; the spins are capped anyway, and
+// a wait that runs out of its cap sets BN_ERR_INTERNAL (the call then fails).
 // (the ring itself, g_lat_ring, is declared in fq12_wide.h beside w12_mul_line)
 __shared__ uint32_t g_lat_prod[kLatPairs], g_lat_cons[kLatPairs], g_lat_skip[kLatPairs];
 __shared__ uint32_t g_lat_duo[kLatPairs * 4];  // BN_FE_DUO: the counters of each pair's channel
@@ -365,13 +357,11 @@ __device__ uint64_t g_lat_stamps[8];
 // the multiplier group of pair j (fq12_wide.h, two-group final exponentiation);
 // its channel is the pair's line ring, free once the Miller loop has read every
 // line -- before S hands over anything
-__device__ __forceinline__ void lat_multiplier(int j, size_t base, size_t n, const uint32_t* f_out) {
-#if BN_WIDE_PAD
+__device__ __forceinline__ void lat_multiplier(int j, size_t base, size_t n, const uint32_t* f_out, int* err) {
+    (void)base;
+    (void)n;
     if (f_out) return;  // no final exponentiation here (idle groups pair up with their idle squarers)
-#else
-    if (f_out || base + j >= n) return;  // no final exponentiation here / no pair
-#endif
-    WDuo duo = {g_lat_ring + j * kLatRing * kLatLineWords, g_lat_duo + 4 * j, 0, 0};
+    WDuo duo = {g_lat_ring + j * kLatRing * kLatLineWords, g_lat_duo + 4 * j, 0, 0, err};
     w12_final_exp_m(duo);
 }
 #endif
@@ -413,8 +403,10 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
             const auto y = narrow<kLine>(fq2_scale(fq2_select(odd_slot, e.ell_vv, e.ell_vw), fq_select(odd_slot, a.px, a.py)));
             const auto x4 = y;
             const auto x2 = pw_from(y, 1);
-            for (uint32_t spins = 0; BN_ANY(valid && line - (int)cons[j] >= kLatRing) && spins < kLatSpinCap; ++spins)
+            uint32_t spins = 0;
+            for (; BN_ANY(valid && line - (int)cons[j] >= kLatRing) && spins < kLatSpinCap; ++spins)
                 __builtin_amdgcn_s_sleep(1);
+            if (spins == kLatSpinCap && L == 0 && err) atomicOr(err, 1 << BN_ERR_INTERNAL);  // ring overrun: fail the call
             asm volatile("" ::: "memory");
             if (st) {  // the operand forms c0, c1, -c1 of each coefficient (fq12_wide.h w12_mul_line)
                 uint32_t* ln = g_lat_ring + (j * kLatRing + line % kLatRing) * kLatLineWords;
@@ -449,33 +441,29 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
         emit(line++, pw_mixed_addition_step(r, q2, k));
         LAT_STAMP(threadIdx.x == 0, 2);  // producer: last line out
 #if BN_FE_DUO
-        lat_multiplier((int)threadIdx.x / kWLanes, base, n, f_out);
+        lat_multiplier((int)threadIdx.x / kWLanes, base, n, f_out, err);
 #endif
         return;
     }
 #if BN_FE_DUO
     if (threadIdx.x >= 64 + kLatPairs * kWLanes) {  // wave 3: the multipliers of pairs 4-7
-        lat_multiplier(kLatPairs / 2 + ((int)threadIdx.x - 64 - kLatPairs * kWLanes) / kWLanes, base, n, f_out);
+        lat_multiplier(kLatPairs / 2 + ((int)threadIdx.x - 64 - kLatPairs * kWLanes) / kWLanes, base, n, f_out, err);
         return;
     }
 #endif
     // ---- consumer groups: pair j on a 16-lane group of waves 1-2
     const int j = ((int)threadIdx.x - 64) / kWLanes;
-#if BN_WIDE_PAD
     // idle groups repeat the block's last pair (the producer fills their rings
     // with it) and store nothing, so a wave runs the same number of groups
     // whatever n is
     const bool live = base + j < n;
     const size_t pi = live ? base + j : n - 1;
-#else
-    const bool live = true;
-    const size_t pi = base + j;
-    if (pi >= n) return;
-#endif
     const WL w = wl();
     auto ln = [&](int line) { return (uint32_t)((j * kLatRing + line % kLatRing) * kLatLineWords); };
     auto wait_line = [&](int line) {
-        for (uint32_t spins = 0; prod[j] <= (uint32_t)line && spins < kLatSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
+        uint32_t spins = 0;
+        for (; prod[j] <= (uint32_t)line && spins < kLatSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
+        if (spins == kLatSpinCap && w.l == 0 && err) atomicOr(err, 1 << BN_ERR_INTERNAL);  // line never published
         asm volatile("" ::: "memory");
     };
     auto took = [&](int line) {  // the line's words have been read (the product has returned)
@@ -490,7 +478,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
 #pragma unroll 1
     for (int d = 0; d < BN_NAF_DIGITS; ++d) {
         if (d > 0) {
-            f = BN_WIDE_SQR ? w12_sqr(f) : w12_mul(f, f);  // the generic square, as the reference's loop
+            f = w12_sqr(f);  // the generic square, as the reference's loop
             wait_line(line);
             f = w12_mul_line(f, ln(line));
             took(line++);
@@ -518,7 +506,7 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
     const bool zero = w12_is_zero(x);
     if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
 #if BN_FE_DUO
-    WDuo duo = {g_lat_ring + j * kLatRing * kLatLineWords, g_lat_duo + 4 * j, 0, 0};
+    WDuo duo = {g_lat_ring + j * kLatRing * kLatLineWords, g_lat_duo + 4 * j, 0, 0, err};
     const Fq<2> res = w12_final_exp_s(x, duo);
 #else
     const Fq<2> res = w12_final_exp(x);
@@ -533,7 +521,10 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
 __global__ void __launch_bounds__(kBlock) k_err_status(const int* __restrict__ err, int* __restrict__ status) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         const int b = *err;
-        *status = (b & (1 << BN_ERR_TO_AFFINE)) ? BN_ERR_TO_AFFINE : (b & (1 << BN_ERR_FE_ZERO)) ? BN_ERR_FE_ZERO : BN_OK;
+        *status = (b & (1 << BN_ERR_INTERNAL))    ? BN_ERR_INTERNAL
+                  : (b & (1 << BN_ERR_TO_AFFINE)) ? BN_ERR_TO_AFFINE
+                  : (b & (1 << BN_ERR_FE_ZERO))   ? BN_ERR_FE_ZERO
+                                                  : BN_OK;
     }
 }
 

@@ -41,14 +41,6 @@ BN_INLINE void g2_precompute(const G2Aff<B>& q, Emit&& emit) {
     emit(k++, mixed_addition_step(r, q2));
 }
 
-#ifndef BN_LINE_ORDER
-// 1 (default): outputs last-first, each xi*f_k made just before its first use; 0:
-// first-first with the four xi*f_k up front.  Under round 1's max-ilp scheduler
-// last-first spilled less but ran 2-3 % slower (profiles/r2ai_ab_line_lazy.txt);
-// under the default scheduler it is faster: k_pairing_fused 4.31 vs 4.34 ms,
-// config 5 2.65 vs 2.70 ms (profiles/r2ax_ab_line_order.txt)
-#define BN_LINE_ORDER 1
-#endif
 #if BN_SPLIT
 // The same product f * (x0 + x4 w^3 + x2 w^4) on the two-lane layout, as six
 // column sums reduced once each.  In the w-basis (f_m = coefficient of w^m:
@@ -60,8 +52,7 @@ BN_INLINE void g2_precompute(const G2Aff<B>& q, Emit&& emit) {
 // reduces once: 36 products + 6 reductions per lane instead of the 13-product
 // formula's 26 + 13, and no combining adds, subtractions or folds.  The line
 // side's operand forms are built once per coefficient.  The value is the
-// reference's product (fq12.rs:130-196) -- the same residues.  BN_LINE_LAZY = 0
-// keeps the 13-product formula (A/B).
+// reference's product (fq12.rs:130-196) -- the same residues.
 struct LineOps {
     Fq<kLine> y;  // v0 on both lanes
     Fq<8> w;      // lane 0: K*p - v1, lane 1: v1 (normalized digits, value <= (kLine + 1) p)
@@ -70,15 +61,12 @@ template <int X>
 BN_INLINE LineOps line_ops(const Fq2<X>& v_in) {
     const Fq<kv(X)> v = fq_norm(v_in.c);
     const bool odd = lane_odd();
-#if defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_DPPSEL
+#if defined(__HIP_DEVICE_COMPILE__)
     // w as fq2_mul_split forms it: the odd lane's own v1, the even lane the partner's K*p - v1
     Fq<kjoin(kv(X), kenc(kv(X) + 1, 2))> w;
     dpp_sel_own_partner(w.v, v.v, fq_neg_lazy(v).v);
     (void)odd;
     return {widen<kLine>(fq_bcast_c0(v)), widen<8>(fq_norm(w))};
-#elif defined(__HIP_DEVICE_COMPILE__) && BN_FQ2_BCAST
-    const Fq<kv(X)> c1 = fq_bcast_c1(v);
-    return {widen<kLine>(fq_bcast_c0(v)), widen<8>(fq_norm(fq_pick(odd, c1, fq_neg_lazy(c1))))};
 #else
     const Fq<kv(X)> pv = fq_partner(v);
     return {widen<kLine>(fq_select(odd, pv, v)), widen<8>(fq_norm(fq_pick(odd, v, fq_neg_lazy(pv))))};
@@ -106,7 +94,9 @@ BN_INLINE Fq12<2> fq12_mul_by_024_lazy(const Fq12<F>& f_in, const Fq2<X>& x0_in,
         acc_mad2(t, c, vc);
         return Fq2<2>{acc_redc<2>(t)};
     };
-#if BN_LINE_ORDER
+    // outputs last-first, each xi*f_k made just before its first use: under the default
+    // scheduler 0.7 % faster than first-first with the four xi*f_k up front
+    // (k_pairing_fused 4.31 vs 4.34 ms, config 5 2.65 vs 2.70 ms, profiles/r2ax_ab_line_order.txt)
     const Fq2<2> o5 = out(f5, x0, f2, x4, f1, x2);
     const Fq2<2> o4 = out(f4, x0, f1, x4, f0, x2);
     const Fq<2> g5 = xi(f5);
@@ -117,26 +107,14 @@ BN_INLINE Fq12<2> fq12_mul_by_024_lazy(const Fq12<F>& f_in, const Fq2<X>& x0_in,
     const Fq2<2> o1 = out(f1, x0, g4, x4, g3, x2);
     const Fq<2> g2 = xi(f2);
     const Fq2<2> o0 = out(f0, x0, g3, x4, g2, x2);
-#else
-    const Fq<2> g2 = xi(f2), g3 = xi(f3), g4 = xi(f4), g5 = xi(f5);
-    const Fq2<2> o0 = out(f0, x0, g3, x4, g2, x2);
-    const Fq2<2> o1 = out(f1, x0, g4, x4, g3, x2);
-    const Fq2<2> o2 = out(f2, x0, g5, x4, g4, x2);
-    const Fq2<2> o3 = out(f3, x0, f0, x4, g5, x2);
-    const Fq2<2> o4 = out(f4, x0, f1, x4, f0, x2);
-    const Fq2<2> o5 = out(f5, x0, f2, x4, f1, x2);
-#endif
     return {{o0, o2, o4}, {o1, o3, o5}};
 }
 #endif
 
-#ifndef BN_LINE_LAZY
-#define BN_LINE_LAZY 1
-#endif
 // f <- f * line(P): ell_vw.scale(Py), ell_vv.scale(Px)  (mod.rs:589)
 template <int B, int PB>
 BN_INLINE Fq12<kF> apply_line(const Fq12<B>& f, const Ell& c, const Fq<PB>& px, const Fq<PB>& py) {
-#if BN_SPLIT && BN_LINE_LAZY
+#if BN_SPLIT
     return widen<kF>(fq12_mul_by_024_lazy(narrow12<2>(f), c.ell_0, narrow<kLine>(fq2_scale(c.ell_vw, py)),
                                           narrow<kLine>(fq2_scale(c.ell_vv, px))));
 #else
@@ -150,9 +128,6 @@ BN_INLINE Fq12<kF> apply_line(const Fq12<B>& f, const Ell& c, const Fq<PB>& px, 
 // operands of apply_line), so the squaring and the sparse product are skipped
 // (k_miller_seg at one pairing, 16 segments: 194 -> 177 us).  The same residues
 // as fq12.rs mul_by_024 applied to Fq12::one().
-#ifndef BN_FIRST_LINE
-#define BN_FIRST_LINE 1
-#endif
 template <int PB>
 BN_INLINE Fq12<kF> line_from_one(const Ell& c, const Fq<PB>& px, const Fq<PB>& py) {
     const Fq2<kF> z = widen<kF>(fq2_zero());
@@ -162,11 +137,7 @@ BN_INLINE Fq12<kF> line_from_one(const Ell& c, const Fq<PB>& px, const Fq<PB>& p
 // f^2 * line, or the line alone on the first step from f = one (wave-uniform `first`)
 template <int PB>
 BN_INLINE Fq12<kF> sqr_line(const Fq12<kF>& f, bool first, const Ell& c, const Fq<PB>& px, const Fq<PB>& py) {
-#if BN_FIRST_LINE
     if (first) return line_from_one(c, px, py);
-#else
-    (void)first;
-#endif
     return apply_line(narrow12<kF>(fq12_sqr(f)), c, px, py);
 }
 

@@ -3,8 +3,8 @@
 // Replaces src/fields/fq2.rs, fq6.rs, fq12.rs.  Each function returns the same
 // residue (mod p, per coefficient) as the reference function it cites; where
 // the formula differs it differs only by a ring identity (x * (p-1) is a
-// negation, x * xi with xi = 9+u is a digit-wise add chain, Fermat instead of
-// binary-Euclid inversion), never in the value.  Formulas that are NOT ring
+// negation, x * xi with xi = 9+u is a digit-wise add chain, binary GCD instead
+// of binary-Euclid inversion), never in the value.  Formulas that are NOT ring
 // identities -- Granger-Scott cyclotomic squaring, the sparse line product --
 // follow the reference's own expressions.
 //
@@ -15,118 +15,10 @@
 #pragma once
 #include "fq.h"
 
-// Fq2 product form used by fq2_mul: 1 = schoolbook with lazy reduction
-// (fq2_mul_sb), 0 = Karatsuba with lazy reduction (fq2_mul_lazy)
-#ifndef BN_FQ2_SB
-#define BN_FQ2_SB 1
-#endif
-// 1: the Fq6 product issues its six Fq2 products as three fenced pairs
-#ifndef BN_FQ6_PAIRS
-#define BN_FQ6_PAIRS 1
-#endif
 
 namespace bn {
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
-
-#ifndef BN_INV_BGCD
-#define BN_INV_BGCD 1  // fq_inv: binary GCD (1) or the Fermat chain (0)
-#endif
-
-// ---------------------------------------------------------------- inversion
-// Fermat: a^(p-2).  Inverses are unique, so this equals the reference's binary
-// extended Euclid (arith.rs:324-370 + fp.rs:108-117) bit for bit, without its
-// data-dependent control flow.  The chain is the windowed plan below (fq_inv_w).
-// ---------------------------------------------------------------- fixed-exponent windowed powers
-// Left-to-right sliding window of width 4 for a constant exponent, planned at
-// compile time as (squarings, odd digit) steps.  The exponent is the same in
-// every lane, so the digit dispatch is a scalar branch.  x^e is unique, so any
-// chain gives the reference's value (fields/mod.rs:35-46 square-and-multiply).
-struct PowPlan {
-    int first = 0, n = 0;
-    uint8_t sq[96] = {};
-    uint8_t dig[96] = {};
-};
-constexpr bool pbit(const uint64_t (&e)[4], int i) { return (e[i >> 6] >> (i & 63)) & 1u; }
-constexpr PowPlan pow_plan(const uint64_t (&e)[4], int top) {
-    PowPlan c;
-    int i = top, pend = 0;
-    bool first = true;
-    while (i >= 0) {
-        if (!pbit(e, i)) {
-            ++pend;
-            --i;
-            continue;
-        }
-        int j = i - 3 < 0 ? 0 : i - 3;
-        while (!pbit(e, j)) ++j;
-        int v = 0;
-        for (int k = i; k >= j; --k) v = 2 * v + (pbit(e, k) ? 1 : 0);
-        if (first) {
-            c.first = v;
-            first = false;
-        } else {
-            c.sq[c.n] = (uint8_t)(pend + i - j + 1);
-            c.dig[c.n] = (uint8_t)v;
-            ++c.n;
-        }
-        pend = 0;
-        i = j - 1;
-    }
-    if (pend) {
-        c.sq[c.n] = (uint8_t)pend;
-        c.dig[c.n] = 0;
-        ++c.n;
-    }
-    return c;
-}
-constexpr uint64_t kPm2[4] = {0x3c208c16d87cfd45ull, 0x97816a916871ca8dull, 0xb85045b68181585dull,
-                              0x30644e72e131a029ull};  // p - 2
-constexpr PowPlan kInvPlan = pow_plan(kPm2, 253);
-
-template <int B>
-BN_INLINE Fq<2> fq_pow_plan(const Fq<B>& a, const PowPlan& c) {
-    const Fq<2> x1 = widen<2>(fq_reduce(a));
-    const Fq<2> x2 = fq_sqr(x1);
-    const Fq<2> x3 = fq_mul(x1, x2), x5 = fq_mul(x3, x2), x7 = fq_mul(x5, x2), x9 = fq_mul(x7, x2);
-    const Fq<2> x11 = fq_mul(x9, x2), x13 = fq_mul(x11, x2), x15 = fq_mul(x13, x2);
-    auto times = [&](const Fq<2>& r, int d) -> Fq<2> {
-        switch (d) {
-            case 1: return fq_mul(r, x1);
-            case 3: return fq_mul(r, x3);
-            case 5: return fq_mul(r, x5);
-            case 7: return fq_mul(r, x7);
-            case 9: return fq_mul(r, x9);
-            case 11: return fq_mul(r, x11);
-            case 13: return fq_mul(r, x13);
-            case 15: return fq_mul(r, x15);
-            default: return r;
-        }
-    };
-    Fq<2> r;
-    switch (c.first) {
-        case 1: r = x1; break;
-        case 3: r = x3; break;
-        case 5: r = x5; break;
-        case 7: r = x7; break;
-        case 9: r = x9; break;
-        case 11: r = x11; break;
-        case 13: r = x13; break;
-        default: r = x15; break;
-    }
-#pragma unroll 1
-    for (int s = 0; s < c.n; ++s) {
-        const int q = c.sq[s];
-#pragma unroll 1
-        for (int k = 0; k < q; ++k) r = fq_sqr(r);
-        r = times(r, c.dig[s]);
-    }
-    return r;
-}
-// Fermat inversion a^(p-2) by the windowed plan (253 squarings, ~55 products
-// instead of the binary chain's ~126): the same unique inverse
-template <int B>
-BN_INLINE Fq<2> fq_inv_w(const Fq<B>& a) { return fq_pow_plan(a, kInvPlan); }
 
 // ---------------------------------------------------------------- binary-GCD inversion
 // Pornin's optimized binary GCD ("Optimized Binary GCD for Modular Inversion",
@@ -141,10 +33,7 @@ BN_INLINE Fq<2> fq_inv_w(const Fq<B>& a) { return fq_pow_plan(a, kInvPlan); }
 // every lane runs the same instructions.  About a third of the instructions of
 // the Fermat chain (253 squarings).  y^-1 is unique, so the value equals the
 // reference's binary extended Euclid (arith.rs:324-370) bit for bit.
-#ifndef BN_INV_ROUNDS
-#define BN_INV_ROUNDS 19
-#endif
-constexpr int kInvRounds = BN_INV_ROUNDS;
+constexpr int kInvRounds = 19;  // ceil((2 * 254 - 1) / 29) = 18, plus one spare
 constexpr Limbs9 kR3 = {{0x0e2312b2u, 0x16c05ca2u, 0x0bc84389u, 0x1cdf310bu, 0x11adafddu, 0x032e568eu, 0x1d6ae48cu,
                          0x10d4cd1fu, 0x0026c2d2u}};  // 2^783 mod p: REDC(v * R^3) = v * R^2
 // (x*f0 + y*g0) / 2^29 for the exact (a, b) update: the low digit cancels; the
@@ -274,13 +163,11 @@ BN_INLINE Fq<2> fq_inv_bgcd(const Fq<B>& x) {
 #endif
     return fq_mul(v, fq_from_limbs<1>(kR3));
 }
+// the inverse is unique, so this equals the reference's binary extended Euclid
+// (arith.rs:324-370 + fp.rs:108-117) bit for bit
 template <int B>
 BN_INLINE Fq<2> fq_inv(const Fq<B>& a) {
-#if BN_INV_BGCD
     return fq_inv_bgcd(a);
-#else
-    return fq_inv_w(a);
-#endif
 }
 // x unchanged when its bound is <= L, else folded to 2 (decided at compile time)
 template <int L, int B>
@@ -351,19 +238,12 @@ BN_INLINE bool fq2_eq(const Fq2<A>& a, const Fq2<B>& b) {
 
 template <int B>
 BN_INLINE Fq2<kv(B)> fq2_norm(const Fq2<B>& a) { return {fq_norm(a.c0), fq_norm(a.c1)}; }
-// BN_FQ2_FENCE = 0 lets the compiler interleave independent Fq2 products
-// (more ILP, more live registers); 1 serializes them in program order.
-#ifndef BN_FQ2_FENCE
-#define BN_FQ2_FENCE 1
-#endif
+// the fences serialize independent Fq2 products in program order (fewer live
+// registers than letting the compiler interleave them)
 template <int B>
 BN_INLINE void fq2_fence(Fq2<B>& a) {
-#if BN_FQ2_FENCE
     fq_fence(a.c0);
     fq_fence(a.c1);
-#else
-    (void)a;
-#endif
 }
 
 template <int B>
@@ -513,11 +393,7 @@ BN_INLINE auto fq2_mul(const Fq2<A>& a_in, const Fq2<B>& b_in) {
     Fq2<B> b = b_in;
     fq2_fence(a);
     fq2_fence(b);
-#if BN_FQ2_SB
-    auto r = fq2_mul_sb(a, b);
-#else
-    auto r = fq2_mul_lazy(a, b);
-#endif
+    auto r = fq2_mul_sb(a, b);  // schoolbook, lazy reduction: 17 % faster than Karatsuba (r1k_fq2_ubench)
     fq2_fence(r);
     return r;
     }
@@ -651,8 +527,8 @@ BN_INLINE auto fq6_mul_by_nonresidue(const Fq6<B>& a) { return mk6(fq2_mul_xi(a.
 template <int A, int B>
 BN_INLINE auto fq6_mul(const Fq6<A>& a, const Fq6<B>& b) {
     if constexpr (kv(A) > 20 || kv(B) > 20) return fq6_mul(pre<20>(a), pre<20>(b)); else {
-#if BN_FQ6_PAIRS
-    // the six Fq2 products in three independent pairs
+    // the six Fq2 products in three independent pairs (one at a time: within noise,
+    // profiles/r3z_ab_fq6_pairs.txt)
     const auto p1 = fq2_mul2(a.c0, b.c0, a.c1, b.c1);
     const auto& a_a = p1.a;
     const auto& b_b = p1.b;
@@ -662,14 +538,6 @@ BN_INLINE auto fq6_mul(const Fq6<A>& a, const Fq6<B>& b) {
     const auto p3 = fq2_mul2(fq2_add(a.c0, a.c1), fq2_add(b.c0, b.c1), fq2_add(a.c0, a.c2), fq2_add(b.c0, b.c2));
     auto t1 = fq2_sub(fq2_sub(p3.a, a_a), b_b);
     auto t2 = fq2_sub(p3.b, a_a);
-#else
-    auto a_a = fq2_mul(a.c0, b.c0);
-    auto b_b = fq2_mul(a.c1, b.c1);
-    auto c_c = fq2_mul(a.c2, b.c2);
-    auto t0 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c1, a.c2), fq2_add(b.c1, b.c2)), b_b), c_c);
-    auto t1 = fq2_sub(fq2_sub(fq2_mul(fq2_add(a.c0, a.c1), fq2_add(b.c0, b.c1)), a_a), b_b);
-    auto t2 = fq2_sub(fq2_mul(fq2_add(a.c0, a.c2), fq2_add(b.c0, b.c2)), a_a);
-#endif
     return mk6(fq2_add(fq2_mul_xi(t0), a_a), fq2_add(t1, fq2_mul_xi(c_c)), fq2_sub(fq2_add(t2, b_b), c_c));
     }
 }

@@ -205,6 +205,30 @@ class _Point:
     def same_image(self, o):
         return type(o) is type(self) and np.array_equal(self.img, o.img)
 
+    # the group law on the engine (bn_{g1,g2}_*_many, lib.rs:388-423, 539-574)
+    def _op(self, op, o=None):
+        return context().group_op_many(self.GROUP, op, self.img, None if o is None else o.img)
+
+    def __add__(self, o):  # mod.rs:294-334
+        return type(self)(self._op("add", o)[0])
+
+    def __sub__(self, o):  # mod.rs:352-358
+        return type(self)(self._op("sub", o)[0])
+
+    def __neg__(self):  # mod.rs:336-350
+        return type(self)(self._op("neg")[0])
+
+    def normalize(self):  # lib.rs:391-398 (in place, as the reference's &mut self)
+        self.img = self._op("normalize")[0]
+
+    def __eq__(self, o):  # PartialEq: projective equality, mod.rs:169-195
+        return type(o) is type(self) and bool(self._op("eq", o)[0])
+
+    def __ne__(self, o):
+        return not self == o
+
+    __hash__ = None
+
 
 _MONT_ONE = _limbs(_RM % P)
 
@@ -212,6 +236,7 @@ _MONT_ONE = _limbs(_RM % P)
 class G1(_Point):
     """Jacobian G1 point (groups::G1, mod.rs:45-50, 371-402)."""
     WIDTH = 12
+    GROUP = "g1"
 
     @classmethod
     def one(cls):  # mod.rs:381-392: (1, 2, 1)
@@ -246,6 +271,7 @@ class G1(_Point):
 class G2(_Point):
     """Jacobian G2 point over Fq2 (groups::G2, mod.rs:408-472)."""
     WIDTH = 24
+    GROUP = "g2"
     _X = (10857046999023057135944570762232829481370756359578518086990519993285655852781,
           11559732032986387107991004021392285783925812861821192530917403151452391805634)
     _Y = (8495653923123431417604973247489272438418190587263600148770280649306958101930,

@@ -19,6 +19,7 @@ BN_ERR_TO_AFFINE = 2
 BN_ERR_FE_ZERO = 3
 BN_ERR_HIP = 4
 BN_ERR_NO_DEVICE = 5
+BN_ERR_INTERNAL = 6
 
 FQ12_OPS = {"mul": 0, "sqr": 1, "inv": 2, "cyc_sqr": 3, "exp_by_neg_z": 4, "frob1": 5, "frob2": 6, "frob3": 7}
 
@@ -35,8 +36,10 @@ EXPORTS = [
     "bn_g1_from_compressed_many_dev", "bn_g2_from_compressed_many_dev", "bn_gt_pow_many", "bn_gt_pow_many_dev",
     "bn_ctx_create_multi", "bn_ctx_num_devices", "bn_ctx_device", "bn_shard_range", "bn_pairing_many_allgather_dev",
     "bn_pairing_batch_dev", "bn_miller_loop_batch_dev", "bn_set_fe_wide_max", "bn_g2_precompute_many",
-    "bn_set_latency_max",
-]
+    "bn_set_latency_max", "bn_dev_status",
+] + ["bn_%s_%s_many%s" % (g, op, dev) for g in ("g1", "g2") for op in ("add", "sub", "neg", "normalize", "eq")
+     for dev in ("", "_dev")]
+GROUP_OPS = ("add", "sub", "neg", "normalize", "eq")
 
 # per-element status (bn_elem_status)
 ST_OK, ST_FIELD_INVALID_SLICE_LENGTH, ST_FIELD_INVALID_U512, ST_FIELD_NOT_MEMBER = 0, 1, 2, 3
@@ -116,7 +119,13 @@ def load():
         "bn_set_fe_wide_max": ([vp, sz], i),
         "bn_set_latency_max": ([vp, sz], i),
         "bn_g2_precompute_many": ([vp, vp, sz, vp], i),
+        "bn_dev_status": ([vp, vp], i),
     }
+    for g in ("g1", "g2"):
+        for op in GROUP_OPS:
+            unary = op in ("neg", "normalize")
+            sig["bn_%s_%s_many" % (g, op)] = ([vp, vp, sz, vp] if unary else [vp, vp, vp, sz, vp], i)
+            sig["bn_%s_%s_many_dev" % (g, op)] = ([vp, vp, sz, vp, vp] if unary else [vp, vp, vp, sz, vp, vp], i)
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
         fn.argtypes = args
@@ -183,7 +192,27 @@ class Context:
         self._check(self._L.bn_pairing_many_allgather_dev(self._h, arr(d_p), arr(d_q), n_per_dev, arr(d_out),
                                                           arr(streams) if streams else None))
 
+    def device(self, k):
+        """Device k's single-device context of a multi-device context (bn_ctx_device):
+        owned by this context, valid while it lives."""
+        h = self._L.bn_ctx_device(self._h, k)
+        if not h:
+            raise BnError(BN_ERR_INVALID_ARGUMENT, "no device %d in this context" % k)
+        sub = Context.__new__(Context)
+        sub._h = ctypes.c_void_p(h)
+        sub._L = self._L
+        sub._owner = self  # keeps the parent (which destroys it) alive
+        return sub
+
+    def dev_status(self, stream=None):
+        """bn_dev_status: synchronize and raise on the sticky device outcome of the
+        status-less _dev calls (BN_ERR_INTERNAL, BN_ERR_FE_ZERO); clears it."""
+        self._check(self._L.bn_dev_status(self._h, stream))
+
     def close(self):
+        if getattr(self, "_owner", None) is not None:  # a device of a multi-device context
+            self._h = None
+            return
         if getattr(self, "_h", None):
             self._L.bn_ctx_destroy(self._h)
             self._h = None
@@ -205,6 +234,28 @@ class Context:
     @property
     def stream(self):
         return self._L.bn_ctx_stream(self._h)
+
+    # ---- group law (lib.rs:388-423, 539-574)
+    def group_op_many(self, group, op, a, b=None):
+        """bn_{g1,g2}_{add,sub,neg,normalize,eq}_many: rows of a (and b); eq returns a
+        uint8 array, the others point images."""
+        w = {"g1": 12, "g2": 24}[group]
+        a = _arr(a, w)
+        args = [self._h, _ptr(a)]
+        if op not in ("neg", "normalize"):
+            b = _arr(b, w)
+            _same_rows(a, b)
+            args.append(_ptr(b))
+        out = np.zeros(a.shape[0], np.uint8) if op == "eq" else np.zeros((a.shape[0], w), np.uint64)
+        self._check(getattr(self._L, "bn_%s_%s_many" % (group, op))(*args, a.shape[0], _ptr(out)))
+        return out
+
+    def group_op_many_dev(self, group, op, d_a, d_b, n, d_out, stream=None):
+        fn = getattr(self._L, "bn_%s_%s_many_dev" % (group, op))
+        if op in ("neg", "normalize"):
+            self._check(fn(self._h, d_a, n, d_out, stream))
+        else:
+            self._check(fn(self._h, d_a, d_b, n, d_out, stream))
 
     # ---- pairing path
     def pairing_many(self, p, q):

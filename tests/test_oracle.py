@@ -184,3 +184,19 @@ def test_pairing_batch_threads_match_shared_loop():
     pz[:] = 0
     pz[:, 4:8] = O.canon_to_mont_array([1])
     assert np.array_equal(O.pairing_batch(pz, q, nthreads=4), gt_one)
+
+
+def test_oracle_group_law_identities():
+    """The oracle's group-law helpers (checkers of tests/test_gpu_group.py) agree with
+    each other: P - P has z = 0, normalize keeps the point and sets z = one,
+    -(-P) is P's image, (P + Q) - Q == P projectively."""
+    p, q, _, _ = O.random_pairs(4, seed=77, nthreads=4)
+    for a, w, add, sub, neg, norm, eq in ((p, 12, O.g1_add, O.g1_sub, O.g1_neg, O.g1_normalize, O.g1_eq),
+                                          (q, 24, O.g2_add, O.g2_sub, O.g2_neg, O.g2_normalize, O.g2_eq)):
+        b = a[::-1].copy()
+        assert not sub(a, a)[:, 2 * w // 3:].any()
+        na = norm(a)
+        assert all(eq(a, na)) and not np.array_equal(na, a)
+        assert np.array_equal(na[:, 2 * w // 3:2 * w // 3 + 4], np.tile(O.canon_to_mont_array([1]).reshape(4), (4, 1)))
+        assert np.array_equal(neg(neg(a)), a)
+        assert all(eq(sub(add(a, b), b), a))
