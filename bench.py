@@ -54,6 +54,11 @@ MAD32_PER_FQMUL = 128  # one 8x32-bit CIOS product: 64 (a*b) + 64 (m*p) v_mad_u6
 # gfx950 integer-VALU peak for v_mad_u64_u32: 4 cycles per wave64 instruction (measured,
 # tools/ubench.hip) = 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz.  ubench sustains 34.7 T/s.
 PEAK_MAD32_PER_S = 256 * 4 * 16 * 2.4e9
+# the same rate as measured: v_mad_u64_u32 issues at 4.77 cycles per wave-instruction with two
+# waves per SIMD (the throughput kernels' occupancy), tools/ubench_mad_issue.hip
+PEAK_MAD32_MEASURED = 256 * 4 * 64 * 2.4e9 / 4.77
+PEAK_MEASURED_SOURCE = ("profiles/r3j_mad_issue.txt: 4.77 cycles per v_mad_u64_u32 wave-instruction at two waves "
+                        "per SIMD (33.0 T/s); `frac` stays against the 4-cycle 39.3 T/s figure")
 PHASES = ["k_prepare", "k_miller", "k_fq12_vm", "k_fe_out"]
 
 
@@ -404,13 +409,13 @@ class GpuEngine:
     """The product path: the engine's C ABI on one MI355X, all work on one real HIP stream."""
     dry = False
 
-    def __init__(self, local_rank):
+    def __init__(self, local_rank, ctx=None):
         import torch
         from substrate_bn import Context
         self.torch = torch
         self.dev = torch.device("cuda", local_rank)
         torch.cuda.set_device(self.dev)
-        self.ctx = Context(local_rank)
+        self.ctx = ctx if ctx is not None else Context(local_rank)
         # one real (non-default) stream for the kernels, torch's copies and the
         # collectives' ordering (handle 0 would mean the context's own stream)
         self.stream = torch.cuda.Stream(self.dev)
@@ -573,30 +578,7 @@ def run_pairing(args, eng, rank, world, dist):
         res["dry_run"] = True
         res["dtype"] = "n/a (dry run: stub engine on CPU, not a pairing)"
     if gpu:
-        per_launch_ms = {PHASES[k]: phase_ms[k] / max(launches, 1) for k in range(4)}
-        fqmul = dict(FQMUL_PER_PAIRING)
-        if per_launch_ms["k_fq12_vm"] < 0.01 * per_launch_ms["k_prepare"]:
-            # miller_form 3: the whole pairing is one kernel (k_pairing_full)
-            per_launch_ms = {"k_pairing_full": per_launch_ms["k_prepare"]}
-            fqmul["k_pairing_full"] = sum(FQMUL_PER_PAIRING.values())
-        elif per_launch_ms["k_miller"] < 0.01 * per_launch_ms["k_prepare"]:
-            # the default form runs to_affine, the line steps and the Miller loop as one
-            # kernel (k_pairing_fused): phase 0 holds both
-            per_launch_ms = {"k_pairing_fused": per_launch_ms["k_prepare"], "k_fq12_vm": per_launch_ms["k_fq12_vm"],
-                             "k_fe_out": per_launch_ms["k_fe_out"]}
-            fqmul["k_pairing_fused"] = FQMUL_PER_PAIRING["k_prepare"] + FQMUL_PER_PAIRING["k_miller"]
-        dom = max(per_launch_ms, key=per_launch_ms.get)
-        achieved = fqmul[dom] * MAD32_PER_FQMUL * chunk / (per_launch_ms[dom] * 1e-3)
-        res["roofline"] = {
-            "bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
-            "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)", "frac": achieved / PEAK_MAD32_PER_S,
-            "traffic": pmc_traffic(dom),
-            "traffic_source": "profiles/pmc_summary.json: HBM bytes per launch from the committed rocprofv3 PMC "
-                              "passes (FETCH_SIZE x2 + WRITE_SIZE), not measured in this run",
-            "kernel": dom, "pairs_per_launch": chunk, "basis": FQMUL_BASIS,
-            "per_launch_ms": {k: round(v, 4) for k, v in per_launch_ms.items()},
-            "whole_pairing_frac": value / world * sum(FQMUL_PER_PAIRING.values()) * MAD32_PER_FQMUL
-            / PEAK_MAD32_PER_S}
+        res["roofline"] = roofline_block(phase_ms, launches, chunk, value / world)
 
     if world > 1:
         # the world size as the communicator sees it: an all-reduce of one per rank
@@ -648,6 +630,139 @@ def run_pairing(args, eng, rank, world, dist):
                                   "matches_hbm_path": bool(np.array_equal(o_h, eng.host(out)))}
     if rank == 0 and world == 1 and args.config == 2 and gpu and not args.no_config4_ref:
         res["config4_on_1_gpu"] = config4_on_one_gpu(args, eng)
+    return res
+
+
+def roofline_block(phase_ms, launches, chunk, per_gpu_value):
+    """The dominant kernel's roofline from the per-phase HIP-event times of one
+    device's bn_pairing_many_dev launches (bn_get_phase_times)."""
+    per_launch_ms = {PHASES[k]: phase_ms[k] / max(launches, 1) for k in range(4)}
+    fqmul = dict(FQMUL_PER_PAIRING)
+    if per_launch_ms["k_fq12_vm"] < 0.01 * per_launch_ms["k_prepare"]:
+        # the default throughput form: the whole pairing is one kernel (k_pairing_full)
+        per_launch_ms = {"k_pairing_full": per_launch_ms["k_prepare"]}
+        fqmul["k_pairing_full"] = sum(FQMUL_PER_PAIRING.values())
+    elif per_launch_ms["k_miller"] < 0.01 * per_launch_ms["k_prepare"]:
+        # the three-launch form 1 runs to_affine, the line steps and the Miller loop as one
+        # kernel (k_pairing_fused, DESIGN.md §4): phase 0 holds both
+        per_launch_ms = {"k_pairing_fused": per_launch_ms["k_prepare"], "k_fq12_vm": per_launch_ms["k_fq12_vm"],
+                         "k_fe_out": per_launch_ms["k_fe_out"]}
+        fqmul["k_pairing_fused"] = FQMUL_PER_PAIRING["k_prepare"] + FQMUL_PER_PAIRING["k_miller"]
+    dom = max(per_launch_ms, key=per_launch_ms.get)
+    achieved = fqmul[dom] * MAD32_PER_FQMUL * chunk / (per_launch_ms[dom] * 1e-3)
+    return {
+        "bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
+        "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)", "frac": achieved / PEAK_MAD32_PER_S,
+        "peak_measured": PEAK_MAD32_MEASURED / 1e12, "frac_of_measured_peak": achieved / PEAK_MAD32_MEASURED,
+        "peak_measured_source": PEAK_MEASURED_SOURCE,
+        "traffic": pmc_traffic(dom),
+        "traffic_source": "profiles/pmc_summary.json: HBM bytes per launch from the committed rocprofv3 PMC "
+                          "passes (FETCH_SIZE x2 + WRITE_SIZE), not measured in this run",
+        "kernel": dom, "pairs_per_launch": chunk, "basis": FQMUL_BASIS,
+        "per_launch_ms": {k: round(v, 4) for k, v in per_launch_ms.items()},
+        "whole_pairing_frac": per_gpu_value * sum(FQMUL_PER_PAIRING.values()) * MAD32_PER_FQMUL / PEAK_MAD32_PER_S}
+
+
+def run_capi_multi(args):
+    """`--form capi`: BASELINE config 4 in ONE process over N devices through the C ABI
+    (SURVEY 8(e) "single process with ncclCommInitAll"): bn_ctx_create_multi over devices
+    0..N-1, device k's HBM-resident shard of rows [k*n, (k+1)*n) (n = --total / N) on
+    device k, and per step one bn_pairing_many_allgather_dev -- every device computes its
+    shard (bn_pairing_many_dev on its own stream), then one grouped RCCL all-gather over
+    xGMI leaves all --total Gt rows on every device in device order.  Timed: a sync of
+    every device on both sides of K steps.  Checked after the timed steps: device 0's
+    gathered rows against the oracle (4,096 rows spread over every shard, the same
+    checker leg as the torch form) and every device's gathered buffer against device 0's.
+    `--dry-run-cpu` runs the control flow with the stub engine (no GPU, no RCCL)."""
+    N = args.gpus
+    total = args.total
+    if total % N:
+        raise SystemExit("config 4: --total %d is not divisible by %d devices" % (total, N))
+    per = total // N
+    dry = args.dry_run_cpu
+    if dry:
+        engs = [DryEngine(k) for k in range(N)]
+        mctx = None
+    else:
+        from substrate_bn import Context
+        mctx = Context(devices=list(range(N)))
+        engs = [GpuEngine(k, ctx=mctx.device(k)) for k in range(N)]
+    torch = engs[0].torch
+    t0 = time.perf_counter()
+    shards = []
+    for k, eng in enumerate(engs):
+        P, Q = eng.points(k * per, per)
+        shards.append((P, Q, eng.empty_gt(total)))
+    for eng in engs:
+        eng.sync()
+    log("capi form: %d devices, %d pairs each, ready in %.1f s" % (N, per, time.perf_counter() - t0))
+
+    def step():
+        if dry:  # the stub: each shard into its slot of every device's buffer ("all-gather")
+            for k, (P, Q, out) in enumerate(shards):
+                engs[k].pairing(P, Q, out[k * per:(k + 1) * per])
+            for j, (_, _, out) in enumerate(shards):
+                for k in range(N):
+                    if j != k:
+                        out[k * per:(k + 1) * per] = shards[k][2][k * per:(k + 1) * per]
+            return
+        mctx.pairing_many_allgather_dev([P.data_ptr() for P, _, _ in shards], [Q.data_ptr() for _, Q, _ in shards],
+                                        per, [o.data_ptr() for _, _, o in shards], [e.sh for e in engs])
+
+    for _ in range(args.warmup):
+        step()
+    for eng in engs:
+        eng.sync()
+    if not dry:
+        for eng in engs:
+            eng.ctx.phase_times()  # discard
+            eng.ctx.set_phase_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    for eng in engs:
+        eng.sync()
+    elapsed = time.perf_counter() - t0
+    value = total * args.steps / elapsed
+    res = {
+        "metric": "BN254 pairings/sec (batched) at 1/2/4/8 MI355X; bit-exact vs CPU ref",
+        "value": value, "unit": "pairings/s", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)",
+        "data": "synthetic: P_j = s_j*G1::one(), Q_j = t_j*G2::one(), s,t uniform Fr images in [1,r), "
+                "SplitMix64 seeds per 4096-row block (substrate_bn/synth.py dataset_scalars)",
+        "config": {"workload": "BASELINE config 4: %d pairings sharded contiguously over %d GPU(s) (%d each) in ONE "
+                               "process (bn_ctx_create_multi) + one RCCL all-gather of all Gt results over xGMI "
+                               "inside the step (bn_pairing_many_allgather_dev)" % (total, N, per),
+                   "total_pairs": total, "pairs_per_gpu": per, "parallelism": "dp%d" % N, "form": "capi",
+                   "chunk": min(per, 1 << 16), "allgather_in_step": True, "inputs": "HBM-resident Jacobian images",
+                   "hbm_io_bytes_per_pairing": 96 + 192 + 384},
+    }
+    if dry:
+        res["dry_run"] = True
+        res["dtype"] = "n/a (dry run: stub engine on CPU, not a pairing)"
+    else:
+        for eng in engs:
+            eng.ctx.set_phase_timing(False)
+        phase_ms, launches = engs[0].ctx.phase_times()
+        for eng in engs[1:]:
+            eng.ctx.phase_times()
+        res["roofline"] = roofline_block(phase_ms, launches, min(per, 1 << 16), value / N)
+        mctx.dev_status()  # the sticky device outcome (BN_ERR_INTERNAL / BN_ERR_FE_ZERO) of every device
+    # every device's gathered buffer equals device 0's
+    ref = shards[0][2]
+    mism = 0
+    for _, _, out in shards[1:]:
+        o = out if dry else out.to(engs[0].dev)
+        mism += int((o != ref).any(dim=1).sum().item())
+    res["collective"] = {"backend": "stub (dry run)" if dry else "rccl: ncclCommInitAll + grouped ncclAllGather "
+                         "(bn_pairing_many_allgather_dev, librccl dlopen'ed)",
+                         "world_from_allreduce": N if dry else mctx.num_devices,
+                         "devices_equal_to_device0": mism == 0, "mismatched_rows": mism,
+                         "what": "the communicator's device count; every device's gathered buffer compared with "
+                                 "device 0's row by row"}
+    if not args.no_cpu_baseline:
+        res["sample_check"], res["cpu_baseline"] = gathered_sample_check(engs[0], ref, total, host_cpus())
     return res
 
 
@@ -714,6 +829,10 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) figure")
     ap.add_argument("--no-config4-ref", action="store_true",
                     help="skip config 4's workload on one GPU (the same-workload N = 1 point) in the N = 1 line")
+    ap.add_argument("--form", choices=["torch", "capi"], default="torch",
+                    help="N > 1 (config 4): torch = one process per GPU over torch.distributed/RCCL (the driver's "
+                         "launch); capi = one process over all N devices through bn_ctx_create_multi + "
+                         "bn_pairing_many_allgather_dev (no ranks spawned)")
     ap.add_argument("--dry-run-cpu", action="store_true",
                     help="control-flow check on CPU: gloo + a stub engine (no pairing is computed)")
     ap.add_argument("--workload", default="pairing",
@@ -725,6 +844,13 @@ def main():
     if args.config is None:
         args.config = 2 if args.gpus == 1 else 4
 
+    if args.form == "capi":
+        if args.workload != "pairing" or os.environ.get("WORLD_SIZE") not in (None, "1"):
+            log("bench: --form capi is config 4 in one process (no launcher, --workload pairing)")
+            return 2
+        args.config = 4
+        print(json.dumps(run_capi_multi(args)), flush=True)
+        return 0
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
         return spawn_ranks(args)

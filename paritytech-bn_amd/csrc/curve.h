@@ -124,16 +124,17 @@ BN_INLINE Jac<F> jac_double(const Jac<F>& s) {
 }
 
 // mod.rs:294-334, including both zero short-cuts and the doubling branch;
-// o_zero = jac_is_zero(o), computed once by a caller that adds the same o often
-template <template <int> class F>
-BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o, bool o_zero) {
+// o_zero = jac_is_zero(o), computed once by a caller that adds the same o often,
+// and z2sq / z2cu = o.z^2, o.z^3 (the same residues whether computed here or
+// once by such a caller: jac_mul's base is fixed, saving 2 of its 16 products)
+template <template <int> class F, class Z2, class Z3>
+BN_INLINE Jac<F> jac_add_pre(const Jac<F>& s, const Jac<F>& o, bool o_zero, const Z2& z2_squared,
+                             const Z3& z2_cubed) {
     const bool s_zero = jac_is_zero(s);
     auto z1_squared = F_sqr(s.z);
-    auto z2_squared = F_sqr(o.z);
     auto u1 = F_mul(s.x, z2_squared);
     auto u2 = F_mul(o.x, z1_squared);
     auto z1_cubed = F_mul(s.z, z1_squared);
-    auto z2_cubed = F_mul(o.z, z2_squared);
     auto s1 = F_mul(s.y, z2_cubed);
     auto s2 = F_mul(o.y, z1_cubed);
     auto h = F_sub(u2, u1);
@@ -154,9 +155,16 @@ BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o, bool o_zero) {
         const bool take = same && !s_zero && !o_zero;
         out = {F_select(take, d.x, out.x), F_select(take, d.y, out.y), F_select(take, d.z, out.z)};
     }
-    out = {F_select(o_zero, s.x, out.x), F_select(o_zero, s.y, out.y), F_select(o_zero, s.z, out.z)};
-    out = {F_select(s_zero, o.x, out.x), F_select(s_zero, o.y, out.y), F_select(s_zero, o.z, out.z)};
+    if (BN_ANY(o_zero || s_zero)) {  // the zero shortcuts (mod.rs:298-304); rare in a chain: wave-uniform guard
+        out = {F_select(o_zero, s.x, out.x), F_select(o_zero, s.y, out.y), F_select(o_zero, s.z, out.z)};
+        out = {F_select(s_zero, o.x, out.x), F_select(s_zero, o.y, out.y), F_select(s_zero, o.z, out.z)};
+    }
     return out;
+}
+template <template <int> class F>
+BN_INLINE Jac<F> jac_add(const Jac<F>& s, const Jac<F>& o, bool o_zero) {
+    const auto z2_squared = F_sqr(o.z);
+    return jac_add_pre(s, o, o_zero, z2_squared, F_mul(o.z, z2_squared));
 }
 
 template <template <int> class F>
@@ -199,6 +207,9 @@ template <template <int> class F, typename Step = NoBitStep>
 BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8], Step&& step = Step{}) {
     Jac<F> res = jac_zero<F>();
     const bool p_zero = jac_is_zero(p);
+    // the base's z^2 and z^3, the same at every addition of the chain
+    const auto pz2 = narrow<kPt>(F_sqr(p.z));
+    const auto pz3 = narrow<kPt>(F_mul(p.z, pz2));
     // lane state: `w` holds the scalar shifted so that the next bit to consume is
     // bit 31 of w[7]; `left` = bits still to consume after the top set bit;
     // `need_add`: the lane's next step is the addition of the current bit
@@ -239,7 +250,7 @@ BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8], Step&& step = Ste
         if (n_add + n_dbl == 0) break;  // wave-uniform
         step(it++);
         if (n_dbl == 0 || 5 * n_add >= 3 * (n_add + n_dbl)) {
-            Jac<F> a = jac_add(res, p, p_zero);
+            Jac<F> a = jac_add_pre(res, p, p_zero, pz2, pz3);
             res = {F_select(need_add, a.x, res.x), F_select(need_add, a.y, res.y), F_select(need_add, a.z, res.z)};
             need_add = false;
         } else {

@@ -126,7 +126,10 @@ def load():
             unary = op in ("neg", "normalize")
             sig["bn_%s_%s_many" % (g, op)] = ([vp, vp, sz, vp] if unary else [vp, vp, vp, sz, vp], i)
             sig["bn_%s_%s_many_dev" % (g, op)] = ([vp, vp, sz, vp, vp] if unary else [vp, vp, vp, sz, vp, vp], i)
+    ab_build = bool(os.environ.get("BN254MI_LIB"))  # an A/B build may predate newer entry points
     for name, (args, res) in sig.items():
+        if ab_build and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res

@@ -57,3 +57,31 @@ def test_sample_blocks_cover_every_shard():
 def test_bench_world_size_must_match_gpus():
     r = run(["--gpus", "2", "--dry-run-cpu"], env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
+
+
+@pytest.mark.parametrize("ndev", [1, 3])
+def test_bench_capi_form_keys(ndev):
+    """`--form capi`: config 4 in one process over N devices (bn_ctx_create_multi +
+    bn_pairing_many_allgather_dev on the GPU); here the stub engine: no ranks are
+    spawned, every device's gathered buffer is compared with device 0's, and rank
+    0's checker sample and cpu_baseline keys are the torch form's."""
+    r = run(["--gpus", str(ndev), "--form", "capi", "--dry-run-cpu", "--steps", "2", "--warmup", "1",
+             "--total", "12288"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "launching" not in r.stderr  # no torch.distributed.run child
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == ndev and line["dry_run"] is True and line["steps"] == 2
+    assert line["config"]["form"] == "capi" and line["config"]["total_pairs"] == 12288
+    assert line["config"]["pairs_per_gpu"] == 12288 // ndev and line["scaling"] == "strong"
+    assert line["collective"]["devices_equal_to_device0"] is True and line["collective"]["world_from_allreduce"] == ndev
+    sc = line["sample_check"]
+    assert sc["mismatches"] == 0 and sc["parity_sample_bit_exact"] is True and sc["last_row"] == 12287
+    assert line["cpu_baseline"]["kind"] == "dry-run stub" and line["value"] > 0
+
+
+def test_bench_capi_form_rejects_launcher_and_workloads():
+    r = run(["--gpus", "2", "--form", "capi", "--dry-run-cpu"], env={"WORLD_SIZE": "2", "RANK": "0",
+                                                                    "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "--form capi" in r.stderr
+    r = run(["--form", "capi", "--workload", "g1mul", "--dry-run-cpu"])
+    assert r.returncode == 2

@@ -103,3 +103,56 @@ def test_torch_distributed_forms_world_of_one(data):
         assert np.array_equal(parallel.pairing_many_distributed(data["pz"], data["q"]), data["gt"])
     finally:
         dist.destroy_process_group()
+
+
+def _device_count():
+    import torch
+    return torch.cuda.device_count()  # does not initialize the GPU runtime on this image
+
+
+needs_two = pytest.mark.skipif(_device_count() < 2, reason="needs two or more visible MI355X")
+
+
+@needs_two
+def test_multi_context_distinct_devices(data):
+    """bn_ctx_create_multi over every visible device: the sharded host calls and the
+    per-device products combined in device order equal the oracle bit for bit."""
+    from substrate_bn import Context
+    nd = _device_count()
+    ctx = Context(devices=list(range(nd)))
+    assert ctx.num_devices == nd
+    assert np.array_equal(ctx.pairing_many(data["pz"], data["q"]), data["gt"])
+    assert np.array_equal(ctx.pairing_batch(data["pz"], data["q"]), data["prod"])
+    _, want = O.miller_loop_batch(data["q"][:33], data["p"][:33])
+    assert np.array_equal(ctx.miller_loop_batch(data["q"][:33], data["p"][:33]), want)
+    ks, K = O.random_scalars(101, seed=911, lo=0)
+    assert np.array_equal(ctx.g1_mul_many(data["p"], K), O.g1_mul(data["p"], K, NT))
+
+
+@needs_two
+def test_allgather_dev_distinct_devices(data):
+    """BASELINE config 4's C-ABI form on real devices: device k computes its HBM-resident
+    shard, one RCCL all-gather (ncclCommInitAll + grouped ncclAllGather) leaves every
+    device holding all rows in device order -- each device's buffer equals the oracle."""
+    import torch
+    from substrate_bn import Context
+    nd = min(_device_count(), 4)
+    per = 101 // nd
+    n = per * nd
+    ctx = Context(devices=list(range(nd)))
+    ins, outs, streams = [], [], []
+    for k in range(nd):
+        dev = torch.device("cuda", k)
+        P = torch.from_numpy(np.ascontiguousarray(data["pz"][k * per:(k + 1) * per]).view(np.int64)).to(dev)
+        Q = torch.from_numpy(np.ascontiguousarray(data["q"][k * per:(k + 1) * per]).view(np.int64)).to(dev)
+        ins.append((P, Q))
+        outs.append(torch.zeros((n, 48), dtype=torch.int64, device=dev))
+        streams.append(torch.cuda.Stream(dev))
+        torch.cuda.synchronize(dev)
+    ctx.pairing_many_allgather_dev([P.data_ptr() for P, _ in ins], [Q.data_ptr() for _, Q in ins], per,
+                                   [o.data_ptr() for o in outs], [s.cuda_stream for s in streams])
+    for k in range(nd):
+        torch.cuda.synchronize(torch.device("cuda", k))
+    ctx.dev_status()
+    for k in range(nd):
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint64), data["gt"][:n]), "device %d" % k

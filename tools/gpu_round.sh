@@ -15,6 +15,9 @@ tail -1 $OUT/gpu_tests.log
 echo "== bench"
 timeout -k 10 300 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
 cat $OUT/bench.json
+echo "== config 4 in one process (bn_ctx_create_multi + bn_pairing_many_allgather_dev; RCCL world of the visible GPUs)"
+timeout -k 10 300 python -u bench.py --form capi --gpus ${CAPI_GPUS:-1} --steps 3 --warmup 1 > $OUT/bench_capi.json 2> $OUT/bench_capi.err
+head -c 400 $OUT/bench_capi.json; echo
 echo "== kernel stats"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py $Q > $OUT/bench_prof.json 2> $OUT/prof.err
 echo "== pmc"
