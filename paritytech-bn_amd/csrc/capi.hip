@@ -462,11 +462,23 @@ int finish_product(bn_ctx* c, const SegPlan& plan, size_t nchunks, int do_fe, bn
 // one-launch k_pairing_latency (no FE), the product reduction, then one group's
 // final exponentiation (do_fe: pairing_batch) or the Miller value itself
 // (miller_loop_batch) into *d_out
+// The one-launch latency kernel over m pairs (out: Gt images, or f_out: the Miller
+// values): the one-wave build while its blocks (8 pairs each, one per CU) fit one
+// round, above that the two-wave build (kernels_latency_w2.hip: two blocks per CU),
+// unless $BN254MI_LATENCY_W2=0 (A/B)
+constexpr size_t kLatW1Max = 2048;
+static void launch_latency(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, bn_gt* out, uint32_t* f_out,
+                           int mode, hipStream_t s) {
+    const unsigned blocks = (unsigned)((m + kLatPairs - 1) / kLatPairs);
+    if (m <= kLatW1Max || !c->latency_w2)
+        k_pairing_latency<<<blocks, kLatThreads, 0, s>>>(d_p, d_q, m, out, f_out, mode, c->d_err);
+    else
+        k_pairing_latency_w2<<<blocks, kLatThreads, 0, s>>>(d_p, d_q, m, out, f_out, mode, c->d_err);
+}
 int latency_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int mode, int do_fe, bn_gt* d_out,
                     hipStream_t s) {
     RET_IF(reserve(c, n));
-    k_pairing_latency<<<(unsigned)((n + kLatPairs - 1) / kLatPairs), kLatThreads, 0, s>>>(
-        d_p, d_q, n, nullptr, slot_region(c, kRegionSeg), mode, c->d_err);
+    launch_latency(c, d_p, d_q, n, nullptr, slot_region(c, kRegionSeg), mode, s);
     HIPCHK(c, hipGetLastError());
     RET_IF(product_wide(c, slot_region(c, kRegionSeg), n, n, n, 1, slot_region(c, kRegionResult), 1, 0, 1, s));
     return recombine_one(c, cut_plan(1, 1), do_fe, d_out, s);  // one segment: the FE of the product when do_fe
@@ -621,6 +633,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
     }
     c->latency_max = kLatencyMaxDefault;
     if (const char* e = getenv("BN254MI_LATENCY_MAX")) c->latency_max = (size_t)strtoull(e, nullptr, 10);
+    if (const char* e = getenv("BN254MI_LATENCY_W2")) c->latency_w2 = atoi(e) != 0;
     c->prepare_wide_max = kPrepareWideMaxDefault;
     if (const char* e = getenv("BN254MI_PREPARE_WIDE_MAX")) c->prepare_wide_max = (size_t)strtoull(e, nullptr, 10);
     Prog P;
@@ -732,8 +745,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
         if (m <= c->fe_wide_max && m <= c->latency_max) {
             // the whole pairing in one launch: line producer + wide Miller loop and FE
             // (kernels_wide.hip k_pairing_latency)
-            k_pairing_latency<<<(unsigned)((m + kLatPairs - 1) / kLatPairs), kLatThreads, 0, s>>>(
-                d_p + off, d_q + off, m, d_out + off, nullptr, 0, c->d_err);
+            launch_latency(c, d_p + off, d_q + off, m, d_out + off, nullptr, 0, s);
             mark(1);
             mark(2);
             mark(3);

@@ -43,6 +43,7 @@ struct bn_ctx {
     int miller_form = 3;  // 3: k_pairing_full; 1: k_pairing_fused + k_fq12_vm + k_fe_out; 0/2: k_prepare + k_miller(_seg) + ...
     // bn_pairing_many_dev batches of at most this many pairs run k_pairing_latency
     size_t latency_max = 0;
+    bool latency_w2 = true;  // above 2,048 pairs the one-launch path runs the two-wave build
     // batches of at most this many pairs take k_prepare_wide (8 lanes per pair)
     size_t prepare_wide_max = 0;
     int* d_err = nullptr;

@@ -31,7 +31,12 @@ static_assert(BN_SPLIT, "fq12_wide.h builds on the two-lane Fq2 of fq2_split.h")
 constexpr int kWLanes = 16;                         // lanes per element (12 hold coordinates)
 constexpr int kWSlot = 12;                          // words per LDS slot: one Fq, 48 B aligned
 constexpr int kWArr = kWLanes * kWSlot;             // words of one operand array of a group
-constexpr int kWArrs = 5;                           // operand arrays per group
+// operand arrays per group: 5 for w12_sqr; 4 (w12_mul only) in the two-wave
+// latency build, whose LDS must fit two blocks per CU (kernels_latency_w2.hip)
+#ifndef BN_WIDE_ARRS
+#define BN_WIDE_ARRS 5
+#endif
+constexpr int kWArrs = BN_WIDE_ARRS;
 constexpr int kWGroupWords = kWArrs * kWArr;        // 3.75 KB per group
 constexpr int kWGroups = kBlock / kWLanes;          // 16 groups per 256-thread block
 __shared__ uint32_t g_wide[kWGroups * kWGroupWords];  // 60 KB
@@ -72,6 +77,15 @@ __device__ __forceinline__ Fq<K> w_get(const uint32_t* arr, int slot) {
     const uint4 a = *(const uint4*)p, b = *(const uint4*)(p + 4);
     return Fq<K>{{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, p[8]}};
 }
+// this lane's coordinate of element e of a lane-strided split Fq12 array
+// (stride = elements in the array)
+__device__ __forceinline__ Fq<2> w_ld_split(const uint32_t* f, size_t stride, size_t e, const WL& w) {
+    return ld_fq<2>(f, 2 * stride, 2 * e + w.c, w_tower_index(w));
+}
+__device__ __forceinline__ void w_st_split(uint32_t* f, size_t stride, size_t e, const WL& w, const Fq<2>& x) {
+    if (w.l < 12) st_fq(f, 2 * stride, 2 * e + w.c, w_tower_index(w), x);
+}
+
 // the writes above are complete before any lane reads (and the compiler keeps order)
 __device__ __forceinline__ void w_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -140,6 +154,7 @@ constexpr uint64_t kWSqrTerm[4] = {
     w_sqr_term(w_sqr_code(3, 3, 3), w_sqr_code(3, 6, 0), w_sqr_code(3, 4, 4), w_sqr_code(3, 6, 0), w_sqr_code(3, 5, 5), w_sqr_code(3, 6, 0)),
 };
 // (squarings as w12_mul(a, a) instead: within 1 %, profiles/r3y_ab_wide_sqr.txt)
+#if BN_WIDE_ARRS >= 5
 __device__ __noinline__ Fq<2> w12_sqr(Fq<2> a) {
     const WL w = wl();
     uint32_t* A_ = w.gb;
@@ -176,12 +191,19 @@ __device__ __noinline__ Fq<2> w12_sqr(Fq<2> a) {
     // value <= 2 * 8 * (2p)^2: the result is below (64 p / 2^261 + 1) p < 2p
     return acc_redc<2>(t);
 }
+__device__ __forceinline__ Fq<2> w12_square(const Fq<2>& a) { return w12_sqr(a); }
+#else
+__device__ __forceinline__ Fq<2> w12_square(const Fq<2>& a) { return w12_mul(a, a); }
+#endif
 
 // Line ring of k_pairing_latency (kernels_wide.hip): per pair kLatRing lines of
 // x0, x4, x2, each stored as the three operand forms of the split product --
 // c0, c1 and -c1 (slots 3q, 3q + 1, 3q + 2; kWSlot words each) -- so a consumer
 // lane reads its two operands with no select or negation
-constexpr int kLatRing = 16;               // lines in flight per pair
+#ifndef BN_LAT_RING
+#define BN_LAT_RING 16
+#endif
+constexpr int kLatRing = BN_LAT_RING;      // lines in flight per pair
 constexpr int kLatLineWords = 9 * kWSlot;  // words per line
 __shared__ uint32_t g_lat_ring[kLatPairs * kLatRing * kLatLineWords];  // 54 KB
 
@@ -451,7 +473,10 @@ constexpr ZNaf z_naf() {
 constexpr ZNaf kZNaf = z_naf();
 static_assert(kZNaf.top == 62 && kZNaf.n == 24, "NAF of u");
 
-constexpr int kDuoRing = 4;                       // S -> M items in flight
+#ifndef BN_DUO_RING
+#define BN_DUO_RING 4
+#endif
+constexpr int kDuoRing = BN_DUO_RING;             // S -> M items in flight
 constexpr int kDuoWords = (kDuoRing + 2) * kWArr;  // channel words per element
 constexpr uint32_t kDuoSpinCap = 1u << 26;        // ~4 s of s_sleep 1: never reached while both run
 

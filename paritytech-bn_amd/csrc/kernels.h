@@ -563,6 +563,10 @@ __global__ void __launch_bounds__(kLatThreads) k_pairing_latency(const bn_g1* __
                                                                  const bn_g2* __restrict__ q, size_t n,
                                                                  bn_gt* __restrict__ out, uint32_t* __restrict__ f_out,
                                                                  int mode, int* __restrict__ err);
+// the same kernel built for two waves per SIMD (kernels_latency_w2.hip)
+__global__ void __launch_bounds__(kLatThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_pairing_latency_w2(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n, bn_gt* __restrict__ out,
+                     uint32_t* __restrict__ f_out, int mode, int* __restrict__ err);
 __global__ void __launch_bounds__(kBlock) k_err_status(const int* __restrict__ err, int* __restrict__ status);
 __global__ void __launch_bounds__(kBlock) k_gt_load(const bn_gt* __restrict__ g, size_t n, uint32_t* __restrict__ f);
 __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict__ f, size_t n, size_t stride, bn_gt* __restrict__ g);
@@ -570,10 +574,10 @@ __global__ void __launch_bounds__(kPairBlock) k_g1_mul(const bn_g1* __restrict__
 __global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g2* __restrict__ out);
 // the group law (kernels_group.hip): op codes of k_g1_op / k_g2_op (b may be null for neg / normalize)
 enum GroupOp { kGroupAdd = 0, kGroupSub = 1, kGroupNeg = 2, kGroupNormalize = 3, kGroupEq = 4 };
-__global__ void __launch_bounds__(kBlock) k_g1_op(int op, const bn_g1* __restrict__ a, const bn_g1* __restrict__ b,
-                                                  size_t n, bn_g1* __restrict__ out, uint8_t* __restrict__ eq);
-__global__ void __launch_bounds__(kBlock) k_g2_op(int op, const bn_g2* __restrict__ a, const bn_g2* __restrict__ b,
-                                                  size_t n, bn_g2* __restrict__ out, uint8_t* __restrict__ eq);
+__global__ void __launch_bounds__(kBlock) k_g1_op(int op, const bn_g1* a, const bn_g1* b, size_t n, bn_g1* out,
+                                                  uint8_t* __restrict__ eq);
+__global__ void __launch_bounds__(kBlock) k_g2_op(int op, const bn_g2* a, const bn_g2* b, size_t n, bn_g2* out,
+                                                  uint8_t* __restrict__ eq);
 __global__ void __launch_bounds__(kPairBlock) k_gt_pow(const bn_gt* __restrict__ a, const bn_fr* __restrict__ k, size_t n,
                                                    bn_gt* __restrict__ out, uint32_t* __restrict__ ws);
 // kernels_codec.hip (codec.h): encodings, square roots, validation, decompression

@@ -80,8 +80,8 @@ __device__ __forceinline__ Jac<F> group_apply(int op, const Jac<F>& x, const Jac
         default: return jac_normalize(x);                     // kGroupNormalize
     }
 }
-__global__ void __launch_bounds__(kBlock) k_g1_op(int op, const bn_g1* __restrict__ a, const bn_g1* __restrict__ b,
-                                                  size_t n, bn_g1* __restrict__ out, uint8_t* __restrict__ eq) {
+__global__ void __launch_bounds__(kBlock) k_g1_op(int op, const bn_g1* a, const bn_g1* b, size_t n, bn_g1* out,
+                                                  uint8_t* __restrict__ eq) {
     fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;
@@ -97,8 +97,8 @@ __global__ void __launch_bounds__(kBlock) k_g1_op(int op, const bn_g1* __restric
     st_ref(out[i].y, r.y);
     st_ref(out[i].z, r.z);
 }
-__global__ void __launch_bounds__(kBlock) k_g2_op(int op, const bn_g2* __restrict__ a, const bn_g2* __restrict__ b,
-                                                  size_t n, bn_g2* __restrict__ out, uint8_t* __restrict__ eq) {
+__global__ void __launch_bounds__(kBlock) k_g2_op(int op, const bn_g2* a, const bn_g2* b, size_t n, bn_g2* out,
+                                                  uint8_t* __restrict__ eq) {
     fold_table_init();
     const size_t i = lane_id();
     if (i >= n) return;

@@ -105,6 +105,12 @@ def test_group_law_dev(ctx, pts, group):
         torch.cuda.synchronize(dev)
         want = ORACLE[group][op](a) if op in ("neg", "normalize") else ORACLE[group][op](a, b)
         assert np.array_equal(out.cpu().numpy().view(np.uint64), want), op
+    # in place (out aliases a): each lane reads its element before it writes it
+    inplace = da.clone()
+    torch.cuda.synchronize(dev)
+    ctx.group_op_many_dev(group, "normalize", inplace.data_ptr(), 0, n, inplace.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert np.array_equal(inplace.cpu().numpy().view(np.uint64), ORACLE[group]["normalize"](a))
     eq = torch.full((n,), 7, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize(dev)
     ctx.group_op_many_dev(group, "eq", da.data_ptr(), db.data_ptr(), n, eq.data_ptr(), s.cuda_stream)

@@ -332,3 +332,33 @@ def test_latency_kernel_1024(ctx, pairs):
     """1024 pairs (the default k_pairing_latency threshold: 128 blocks) bit-exact."""
     p, q, _, _ = O.random_pairs(1024, seed=1025, nthreads=NT)
     assert np.array_equal(ctx.pairing_many(p, q), O.pairing_many(p, q, NT))
+
+
+@pytest.fixture(scope="module")
+def ctx_w2():
+    """A context whose one-launch latency path reaches 4,096 pairs: above 2,048 it
+    runs the two-wave build k_pairing_latency_w2 (kernels_latency_w2.hip)."""
+    from substrate_bn import Context
+    c = Context(0)
+    c.set_latency_max(4096)
+    return c
+
+
+@pytest.mark.parametrize("n", [2049, 3001, 4096])
+def test_latency_kernel_two_wave_build(ctx_w2, n):
+    """k_pairing_latency_w2 (two blocks per CU: six-line ring, one-item FE channel,
+    squarings by w12_mul) bit-exact against the oracle, with zero points on both
+    sides and a partial last block; pairing_batch and miller_loop_batch take the
+    same kernel for their Miller values (f_out mode)."""
+    p, q, _, _ = O.random_pairs(n, seed=7000 + n, nthreads=NT)
+    one = O.canon_to_mont_array([1])
+    p[n - 1] = 0
+    p[n - 1, 4:8] = one
+    q[5] = 0
+    q[5, 8:12] = one
+    want = O.pairing_many(p, q, NT)
+    assert np.array_equal(ctx_w2.pairing_many(p, q), want)
+    if n == 3001:
+        assert np.array_equal(ctx_w2.pairing_batch(p, q), O.pairing_batch(p, q))
+        _, mlb = O.miller_loop_batch(q[6:n - 1], p[6:n - 1])  # rows without a zero point
+        assert np.array_equal(ctx_w2.miller_loop_batch(q[6:n - 1], p[6:n - 1]), mlb)

@@ -35,4 +35,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_g1mul -o run -- 
 echo "== latency"
 timeout -k 10 300 python -u tools/latency.py --calls pairing_many_dev,pairing_many,pairing_batch --sizes 1,2,8,64,256,1024,2048,4096 > $OUT/latency.jsonl 2> $OUT/latency.err
 head -3 $OUT/latency.jsonl
+echo "== latency 2049-4096: one-launch two-wave build vs one-wave build (two rounds) vs segmented"
+timeout -k 10 300 python -u tools/latency.py --calls pairing_many_dev,pairing_batch --sizes 2049,3072,4096 --latency-max 4096 > $OUT/latency_w2.jsonl 2> $OUT/latency_w2.err
+BN254MI_LATENCY_W2=0 timeout -k 10 300 python -u tools/latency.py --calls pairing_many_dev --sizes 2049,4096 --latency-max 4096 > $OUT/latency_w1.jsonl 2> $OUT/latency_w1.err
+grep -h '"n"' $OUT/latency_w2.jsonl $OUT/latency_w1.jsonl | cut -c1-120
 echo "== done"
