@@ -203,13 +203,13 @@ def gathered_sample_check(eng, rows_all, total, cpus, single=256):
     return check, base
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, key="hbm_bytes_per_launch"):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary, if any."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+        return d.get(kernel, {}).get(key)
     except (OSError, ValueError):
         return None
 
@@ -260,6 +260,9 @@ def other_workload(args, local_rank):
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     res.update({"metric": unit, "value": n * args.steps / el, "unit": unit, "ms_per_step": el / args.steps * 1e3})
+    if args.no_cpu_baseline:  # profiler passes: the kernels only
+        print(json.dumps(res), flush=True)
+        return
     from oracle import oracle as O  # the checker (cpu_baseline leg)
     if args.workload == "product":
         # SURVEY 8(d) config 5 algorithmic work: per term to_affine 19 + precompute 2,655 + lines 3,741
@@ -268,8 +271,13 @@ def other_workload(args, local_rank):
         ms = e0.elapsed_time(e1) / args.steps
         res["roofline"] = {"bound": "valu", "achieved": work / (ms * 1e-3) / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
                            "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)",
-                           "frac": work / (ms * 1e-3) / PEAK_MAD32_PER_S, "traffic": None,
-                           "kernel": "whole product (k_prepare, k_miller, k_fq12_reduce_wide x2, k_fe_wide)",
+                           "frac": work / (ms * 1e-3) / PEAK_MAD32_PER_S,
+                           "traffic": pmc_traffic("product_step", "hbm_bytes_per_step"),
+                           "traffic_source": "profiles/pmc_summary.json product_step: FETCH_SIZE (read-factor "
+                                             "corrected) + WRITE_SIZE of every kernel of one product, committed "
+                                             "rocprofv3 PMC passes, not measured in this run",
+                           "kernel": "whole product (k_prepare_wide, k_miller_seg, k_fq12_reduce_wide x3, "
+                                     "k_horner_tree)",
                            "per_step_ms": ms,
                            "basis": "SURVEY.md 8(d) config 5: n*(19+2655+3741) + 2304 + 8767 Fq-mul, x128 MAD32"}
         threads = host_cpus()["usable"]
@@ -299,9 +307,11 @@ def other_workload(args, local_rank):
                            "traffic_source": "profiles/pmc_summary.json (committed PMC run, not this run)",
                            "kernel": "k_g1_mul", "per_launch_ms": ms,
                            "basis": "SURVEY.md 8(d) config 3: 3,800 Fq-mul per G1*Fr, x128 MAD32",
-                           "executed": "the reference chain on every lane: each of the 256 bits runs the doubling "
-                                       "(7 Fq-mul) and, when any lane of the wave has the bit set, the masked "
-                                       "addition (16 Fq-mul) -- ~5,800 Fq-mul executed per lane for random scalars"}
+                           "executed": "the reference chain on every lane, ballot-scheduled: each iteration of a wave runs "
+                                       "either the doubling (7 Fq-mul) or the addition (14 Fq-mul: the base's z^2 "
+                                       "and z^3 are computed once per chain) for the lanes whose next step it is "
+                                       "-- ~5,000 Fq-mul-weighted steps per lane for random scalars (1.4x the "
+                                       "basis: lanes of a wave wait for each other's step kind)"}
         m = min(args.cpu_sample or 2048, n)
         threads = host_cpus()["usable"]
         ph, kh, oh = (t[:m].cpu().numpy().view(np.uint64) for t in (P, k2, out))
@@ -747,7 +757,8 @@ def run_capi_multi(args):
         phase_ms, launches = engs[0].ctx.phase_times()
         for eng in engs[1:]:
             eng.ctx.phase_times()
-        res["roofline"] = roofline_block(phase_ms, launches, min(per, 1 << 16), value / N)
+        # the C ABI cuts each device's shard into its own launch chunks: pairs per launch from the count
+        res["roofline"] = roofline_block(phase_ms, launches, per * args.steps // max(launches, 1), value / N)
         mctx.dev_status()  # the sticky device outcome (BN_ERR_INTERNAL / BN_ERR_FE_ZERO) of every device
     # every device's gathered buffer equals device 0's
     ref = shards[0][2]

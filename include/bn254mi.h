@@ -247,8 +247,10 @@ int bn_set_fe_wide_max(bn_ctx* ctx, size_t n);
 /* Within the latency path, bn_pairing_many_dev batches of at most n pairs run the
  * whole pairing in ONE launch (k_pairing_latency: a wave computing the 87 lines of
  * each pair feeds, through an LDS ring, 16-lane groups running the Miller loop and
- * the final exponentiation); larger ones the segmented three-kernel form.
- * Default 2048 or $BN254MI_LATENCY_MAX; 0 disables it; results are identical. */
+ * the final exponentiation; above 2,048 pairs its two-wave build, two blocks per CU);
+ * larger ones the segmented three-kernel form.  pairing_batch / miller_loop_batch take
+ * the same kernel for their Miller values up to n pairs.
+ * Default 4096 or $BN254MI_LATENCY_MAX; 0 disables it; results are identical. */
 int bn_set_latency_max(bn_ctx* ctx, size_t n);
 /* device milliseconds per phase of bn_pairing_many_dev since the last read, per chunk
  * launch set: the default throughput form is one kernel (k_pairing_full) and the

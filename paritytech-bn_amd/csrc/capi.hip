@@ -66,7 +66,9 @@ constexpr size_t kFeWideMaxDefault = 8192;
 // batches up to this size run the one-launch latency kernel (k_pairing_latency:
 // a line-producer wave feeding the wide Miller loop and final exponentiation);
 // BN254MI_LATENCY_MAX or bn_set_latency_max override (0: never)
-constexpr size_t kLatencyMaxDefault = 2048;  // crossover: 2048 pairs 1.27 vs 1.92 ms, 4096 2.46 vs 1.94 ms (profiles/r3e_latency.jsonl)
+// (above 2,048 pairs the two-wave build k_pairing_latency_w2: 4,096 pairs 1.60 ms against 1.94 ms for
+// the segmented path and 2.18 ms for the one-wave build's two rounds, profiles/r4a_latency_w2_vs_w1.jsonl)
+constexpr size_t kLatencyMaxDefault = 4096;  // one-wave crossover: 2048 pairs 1.27 vs 1.92 ms (profiles/r3e_latency.jsonl)
 // batches up to this size run k_prepare_wide (8 lanes per pair: 2^14 pairs fill
 // the GPU at two waves per SIMD).  BN254MI_PREPARE_WIDE_MAX overrides (0: never).
 constexpr size_t kPrepareWideMaxDefault = 16384;

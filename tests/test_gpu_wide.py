@@ -159,17 +159,17 @@ def test_product_across_chunks_is_one(ctx):
 
 @pytest.mark.parametrize("tree", ["1", "0"])
 def test_segmented_product_recombination(ctx, tree, monkeypatch):
-    """Products above the one-launch size (2,500 terms: prepare + 16 segments of
+    """Products above the one-launch size (4,500 terms: prepare + 16 segments of
     the shared-squaring loop + reduction) through both recombination kernels:
     k_horner_tree (the segments' squarings side by side, then a product tree;
     default) and k_horner_wide (Horner's rule on one group, BN254MI_HORNER_TREE=0)
     -- pairing_batch and miller_loop_batch (no final exponentiation) bit-exact
     against the oracle (mod.rs:609-640, 904-926)."""
     monkeypatch.setenv("BN254MI_HORNER_TREE", tree)
-    n = 2500
+    n = 4500
     p, q, _, _ = O.random_pairs(n, seed=77, nthreads=NT)
-    p[2300] = 0  # a zero point: skipped by pairing_batch (outside the miller_loop_batch slice)
-    p[2300, 4:8] = O.canon_to_mont_array([1])
+    p[4400] = 0  # a zero point: skipped by pairing_batch (outside the miller_loop_batch slice)
+    p[4400, 4:8] = O.canon_to_mont_array([1])
     assert np.array_equal(ctx.pairing_batch(p, q), O.pairing_batch(p, q, nthreads=NT))
-    rc, want = O.miller_loop_batch(q[:2100], p[:2100])
-    assert rc == 0 and np.array_equal(ctx.miller_loop_batch(q[:2100], p[:2100]), want)
+    rc, want = O.miller_loop_batch(q[:4200], p[:4200])
+    assert rc == 0 and np.array_equal(ctx.miller_loop_batch(q[:4200], p[:4200]), want)

@@ -25,6 +25,11 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o p -- python3
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_write.err
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_sq -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_sq.err
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU -d $OUT/pmc_sq2 -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_sq2.err
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_prod_fetch -o p -- python3 bench.py --workload product --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_prod_fetch.err
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_prod_write -o p -- python3 bench.py --workload product --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_prod_write.err
+timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_g1_fetch -o p -- python3 bench.py --workload g1mul --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_g1_fetch.err
+timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_g1_write -o p -- python3 bench.py --workload g1mul --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_g1_write.err
+timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_g1_sq -o p -- python3 bench.py --workload g1mul --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_g1_sq.err
 echo "== workloads"
 for w in g1mul product gtpow g2validate g2decompress; do
   timeout -k 10 300 python -u bench.py --workload $w --steps 10 --warmup 2 > $OUT/bench_$w.json 2> $OUT/bench_$w.err

@@ -60,7 +60,14 @@ if db is not None:
 
 # ---- PMC passes
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
+prod = collections.defaultdict(lambda: collections.defaultdict(list))  # the config-5 product's kernels
+for sub in ("pmc_prod_fetch", "pmc_prod_write"):
+    db = one_db(sub + "/*results.db")
+    if db is None:
+        continue
+    for kname, cname, val in db.execute("select kernel_name, counter_name, value from counters_collection"):
+        prod[short(kname)][cname].append(float(val))
+for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_g1_fetch", "pmc_g1_write", "pmc_g1_sq"):
     db = one_db(sub + "/*results.db")
     if db is None:
         continue
@@ -130,7 +137,31 @@ for k, v in sorted(agg.items()):
                           + factor_src + "), "
                           "WRITE_SIZE as counted (MI355X_MICROARCH §HBM); source %s" % tag}
     lines.append("%-16s %14.3e %14.3e %14.3e %12.3e %10.3f" % (k, fetch, write, valu, cyc, valu / cyc if cyc else 0))
+if prod:
+    # one product step = one k_horner_tree launch; its traffic is every launch's bytes in the pass
+    steps = len(prod.get("k_horner_tree", {}).get("FETCH_SIZE", [])) or 1
+    per_kernel = {}
+    product_kernels = ("k_prepare_wide", "k_prepare", "k_miller_seg", "k_fq12_reduce_wide", "k_horner_tree",
+                       "k_horner_wide", "k_pairing_latency", "k_err_status")  # not the bench's input generation
+    for k, v in prod.items():
+        if k not in product_kernels:
+            continue
+        f = sum(v.get("FETCH_SIZE", [])) * 1024 / steps
+        w = sum(v.get("WRITE_SIZE", [])) * 1024 / steps
+        per_kernel[k] = {"fetch_bytes_raw": f, "write_bytes": w,
+                         "hbm_bytes": (f / read_factor if read_factor else f) + w}
+    summary["product_step"] = {
+        "hbm_bytes_per_step": sum(x["hbm_bytes"] for x in per_kernel.values()), "per_kernel": per_kernel,
+        "steps_in_pass": steps, "read_factor": read_factor, "read_factor_source": factor_src,
+        "note": "config 5 (bench.py --workload product): FETCH_SIZE (corrected by the read factor) + WRITE_SIZE of "
+                "every kernel of one pairing_batch_dev call; source %s" % tag}
+    print("product step: %.3e HBM bytes (%s)" % (summary["product_step"]["hbm_bytes_per_step"],
+                                                ", ".join("%s %.2e" % (k, v["hbm_bytes"]) for k, v in per_kernel.items())))
 if summary:
+    if os.path.exists(prev):  # keep the entries of kernels this session did not profile
+        old = json.load(open(prev))
+        old.update(summary)
+        summary = old
     json.dump(summary, open(os.path.join(out_dir, "pmc_summary.json"), "w"), indent=1)
     open(os.path.join(out_dir, "%s_pmc.txt" % tag), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
