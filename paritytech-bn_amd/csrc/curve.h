@@ -194,6 +194,25 @@ BN_INLINE Jac<F> jac_neg(const Jac<F>& a) {
 // every lane, round 2) executes 253 x (7 + 16) Fq-mul per lane for
 // random scalars; the scheduled chain ~8 % less (a simulation of 64 random
 // 254-bit scalars: 5,302 against 5,819 Fq-mul-weighted steps).
+// Diagnostic build (-DBN_MUL_STATS=1, tools/mul_stats.py): per iteration of the
+// ballot loop, the first lane of the wave adds to g_mul_stats[0/1] the additions /
+// doublings run, [2/3] the lanes they served and [4] the unfinished lanes -- the
+// measured lane occupancy of the schedule.  The product build has none of it.
+#if defined(BN_MUL_STATS) && BN_MUL_STATS && defined(__HIPCC__)
+__device__ unsigned long long g_mul_stats[5];
+#endif
+#if defined(BN_MUL_STATS) && BN_MUL_STATS && defined(__HIP_DEVICE_COMPILE__)
+#define BN_MUL_STAT(is_add, served, live)                                                  \
+    do {                                                                                   \
+        if (__lane_id() == (unsigned)__ffsll(__ballot(1)) - 1) {                           \
+            atomicAdd(&g_mul_stats[(is_add) ? 0 : 1], 1ull);                               \
+            atomicAdd(&g_mul_stats[(is_add) ? 2 : 3], (unsigned long long)(served));       \
+            atomicAdd(&g_mul_stats[4], (unsigned long long)(live));                        \
+        }                                                                                  \
+    } while (0)
+#else
+#define BN_MUL_STAT(is_add, served, live) ((void)0)
+#endif
 #if defined(__HIP_DEVICE_COMPILE__)
 #define BN_BALLOT_COUNT(p) ((uint32_t)__popcll(__ballot((int)(p))))
 #else
@@ -249,7 +268,9 @@ BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8], Step&& step = Ste
         const uint32_t n_add = BN_BALLOT_COUNT(need_add), n_dbl = BN_BALLOT_COUNT(need_dbl);
         if (n_add + n_dbl == 0) break;  // wave-uniform
         step(it++);
-        if (n_dbl == 0 || 5 * n_add >= 3 * (n_add + n_dbl)) {
+        const bool do_add = n_dbl == 0 || 5 * n_add >= 3 * (n_add + n_dbl);
+        BN_MUL_STAT(do_add, do_add ? n_add : n_dbl, n_add + n_dbl);
+        if (do_add) {
             Jac<F> a = jac_add_pre(res, p, p_zero, pz2, pz3);
             res = {F_select(need_add, a.x, res.x), F_select(need_add, a.y, res.y), F_select(need_add, a.z, res.z)};
             need_add = false;

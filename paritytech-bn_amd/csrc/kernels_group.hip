@@ -118,3 +118,12 @@ __global__ void __launch_bounds__(kBlock) k_g2_op(int op, const bn_g2* a, const 
 }  // namespace bn
 
 BN_EXPORT_FOLD_CHECK(group)
+
+#if defined(BN_MUL_STATS) && BN_MUL_STATS
+// the G*Fr schedule counters of the diagnostic build (curve.h BN_MUL_STAT), read and cleared
+extern "C" int bn_dbg_mul_stats(unsigned long long out[5]) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bn::g_mul_stats), 5 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    const unsigned long long z[5] = {0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(bn::g_mul_stats), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
