@@ -397,30 +397,23 @@ static SegPlan cut_plan(int S, int K) {
 // at 4096 through the longer Horner recombination of every pair)
 SegPlan seg_plan(size_t n) {
     int S = 1;
-    while (S < 16 && (size_t)S * n < ((size_t)1 << 16) && !(S >= 8 && (size_t)S * n >= ((size_t)1 << 14))) S *= 2;
+    while (S < kMaxSeg && (size_t)S * n < ((size_t)1 << 16) && !(S >= 8 && (size_t)S * n >= ((size_t)1 << 14))) S *= 2;
     return cut_plan(S, 1);
 }
-// pairing_batch / miller_loop_batch (one recombination for the whole product):
-// kBatchSeg segments, and K pairs per lane pair sharing one squaring per digit
-// (mod.rs:609-640) -- the largest K <= 16 that still leaves S * ceil(n/K) >= 2^16
-// lane pairs (two waves per SIMD).  At 2^14 terms: 32 segments, K = 8 -- a lane
-// pair runs 2 digits with one squaring and ~10.9 lines each (16 segments, K = 4:
-// 4 digits, ~5.4 lines each, twice the squarings).  $BN254MI_BATCH_SEGS (16 or 32)
-// and $BN254MI_BATCH_K override (A/B).
-constexpr int kBatchSeg = 32;
+// pairing_batch / miller_loop_batch (one Horner recombination for the whole
+// product): 16 segments, and K pairs per lane pair sharing one squaring per
+// digit (mod.rs:609-640) -- the largest K <= 16 that still leaves 16 * ceil(n/K)
+// >= 2^16 lane pairs (two waves per SIMD).  At 2^14 terms: K = 4, a lane pair
+// runs 4 digits with one squaring and ~5.3 lines each instead of 16 digits
+// with one squaring and ~1.3 lines each (S = 4, K = 1 before).
 SegPlan batch_plan(size_t n) {
-    int S = kBatchSeg;
-    if (const char* e = getenv("BN254MI_BATCH_SEGS")) {
-        const int v = atoi(e);
-        if (v == 16 || v == 32) S = v;
-    }
     int K = 1;
-    while (K < 16 && (size_t)S * ((n + 2 * K - 1) / (2 * K)) >= ((size_t)1 << 16)) K *= 2;
+    while (K < 16 && (size_t)kMaxSeg * ((n + 2 * K - 1) / (2 * K)) >= ((size_t)1 << 16)) K *= 2;
     if (const char* e = getenv("BN254MI_BATCH_K")) {  // A/B: pairs per lane pair (1, 2, 4, 8, 16)
         const int v = atoi(e);
         if (v >= 1 && v <= 16) K = v;
     }
-    return cut_plan(S, K);
+    return cut_plan(kMaxSeg, K);
 }
 
 // Segment values of m <= kChunk device pairs (mode 0: a pair with a zero point

@@ -489,7 +489,7 @@ inline void vm_step(uint32_t out[2], uint32_t op, uint32_t d, uint32_t a, uint32
 
 // Segments of the Miller loop's 64 NAF digits (k_miller_seg / k_horner_wide):
 // segment s covers digits [lo[s], hi[s]) and starts at line coefficient idx[s]
-constexpr int kMaxSeg = 32;  // SegPlan capacity; pairing_batch runs 32 segments, the latency path <= 16
+constexpr int kMaxSeg = 16;
 // K: pairs per lane pair -- the reference's shared-squaring multi-Miller loop
 // (mod.rs:609-640): lane pair g of a segment squares its accumulator once per
 // digit and multiplies in the lines of pairs g, g + G, ..., g + (K-1) G

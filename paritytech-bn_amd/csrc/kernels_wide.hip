@@ -211,8 +211,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
 }
 
 // The same recombination for ONE element (n = 1: the product of pairing_batch /
-// miller_loop_batch) on the 16 groups of one block, as a tree (S <= 32: above 16
-// segments each group first combines two by Horner's rule).  Horner's
+// miller_loop_batch) on the S <= 16 groups of one block, as a tree.  Horner's
 // value f = (..(g_0^(2^len_1) g_1)^(2^len_2)..)^(2^len_(S-1)) g_(S-1) is the
 // product over s of g_s^(2^e_s), e_s = len_(s+1) + .. + len_(S-1), because
 // squaring is a ring homomorphism; so group s loads g_s and squares it e_s times,
@@ -245,24 +244,13 @@ __global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restri
     w_duo_init();
     const WL w = wl();
     const int grp = (int)threadIdx.x / kWLanes;
-    // up to 32 segments: group g takes segments per*g .. per*g + per - 1 and first
-    // combines a pair by Horner's rule, x = g_a^(2^len_b) * g_b (generic squarings:
-    // raw Miller values), then carries on as the combined segment
-    const int per = plan.S > kWGroups ? 2 : 1;
-    const int ngrp = (plan.S + per - 1) / per;  // groups holding segments
-    const int s0 = grp * per;
-    const bool seg = grp < ngrp;
+    const bool seg = grp < plan.S;
     Fq<2> x = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
-    if (seg) x = w_ld_split(g, (size_t)plan.S, (size_t)s0, w);
-    if (seg && per == 2 && s0 + 1 < plan.S) {
-#pragma unroll 1
-        for (int k = plan.lo[s0 + 1]; k < plan.hi[s0 + 1]; ++k) x = w12_square(x);
-        x = w12_mul(x, w_ld_split(g, (size_t)plan.S, (size_t)(s0 + 1), w));
-    }
+    if (seg) x = w_ld_split(g, (size_t)plan.S, (size_t)grp, w);
     int e = 0, e0 = 0;  // this group's squarings (g_s^(2^e_s)) and group 0's (the most)
-    for (int t = per; t < plan.S; ++t) {
+    for (int t = 1; t < plan.S; ++t) {
         e0 += plan.hi[t] - plan.lo[t];
-        if (t >= s0 + per) e += plan.hi[t] - plan.lo[t];
+        if (t > grp) e += plan.hi[t] - plan.lo[t];
     }
     HOR_STAMP(1);  // g_0 in
     if (do_fe) {
@@ -288,7 +276,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restri
         w_put(mine, w.l, x);
         __syncthreads();
         const Fq<2> y = w12_mul(x, w_get<2>(g_wval + (((grp + h) % kWGroups) * kWLanes) * kWSlot, w.l));
-        if (grp < h && grp + h < ngrp) x = y;  // groups past the segments hold one
+        if (grp < h && grp + h < plan.S) x = y;  // groups past S hold one
         __syncthreads();
     }
     // every group takes group 0's value: the pairs (g, g + 8) run the last chunk side by side

@@ -37,6 +37,11 @@ for w in g1mul product gtpow g2validate g2decompress; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_product -o run -- python3 bench.py --workload product --steps 10 > /dev/null 2> $OUT/prof_product.err
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_g1mul -o run -- python3 bench.py --workload g1mul --steps 5 --cpu-sample 64 > /dev/null 2> $OUT/prof_g1mul.err
+if [ -f exp/lib_mulstats.so ]; then
+  echo "== G*Fr schedule counters (diagnostic build)"
+  BN254MI_LIB=exp/lib_mulstats.so timeout -k 10 120 python -u tools/mul_stats.py > $OUT/mul_stats.json 2> $OUT/mul_stats.err
+  cat $OUT/mul_stats.json
+fi
 echo "== latency"
 timeout -k 10 300 python -u tools/latency.py --calls pairing_many_dev,pairing_many,pairing_batch --sizes 1,2,8,64,256,1024,2048,4096 > $OUT/latency.jsonl 2> $OUT/latency.err
 head -3 $OUT/latency.jsonl
