@@ -214,6 +214,9 @@ def pmc_traffic(kernel, key="hbm_bytes_per_launch"):
         return None
 
 
+G1_MUL2_MIN_LANES = 256 * 512  # capi.hip g1_mul_launch: k_g1_mul2 from this many lanes (kG1MulPairBlockMin)
+
+
 def other_workload(args, local_rank):
     """BASELINE config 3 (batched G1 * Fr) and config 5 (pairing product), 1 GPU."""
     import torch
@@ -301,25 +304,33 @@ def other_workload(args, local_rank):
         # x 16), x128 MAD32; the kernel is the only launch of the step (HIP events on its stream)
         ms = e0.elapsed_time(e1) / args.steps
         work = n * 3800 * MAD32_PER_FQMUL
+        g1_kernel = "k_g1_mul2" if (n + 1) // 2 >= G1_MUL2_MIN_LANES else "k_g1_mul"
         res["roofline"] = {"bound": "valu", "achieved": work / (ms * 1e-3) / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
                            "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)",
-                           "frac": work / (ms * 1e-3) / PEAK_MAD32_PER_S, "traffic": pmc_traffic("k_g1_mul"),
+                           "frac": work / (ms * 1e-3) / PEAK_MAD32_PER_S, "traffic": pmc_traffic(g1_kernel),
                            "traffic_source": "profiles/pmc_summary.json (committed PMC run, not this run)",
-                           "kernel": "k_g1_mul", "per_launch_ms": ms,
+                           "kernel": g1_kernel,
+                           "per_launch_ms": ms,
                            "basis": "SURVEY.md 8(d) config 3: 3,800 Fq-mul per G1*Fr, x128 MAD32",
-                           "executed": "the reference chain on every lane, ballot-scheduled: each iteration of a wave runs "
-                                       "either the doubling (7 Fq-mul) or the addition (14 Fq-mul: the base's z^2 "
-                                       "and z^3 are computed once per chain) for the lanes whose next step it is "
-                                       "-- ~5,000 Fq-mul-weighted steps per lane for random scalars (1.4x the "
-                                       "basis: lanes of a wave wait for each other's step kind)"}
+                           "executed": "the reference chain of every multiplication, ballot-scheduled: from 2^18 - 1 "
+                                       "multiplications on, each lane runs two chains (rows i and i + n/2) and every "
+                                       "iteration of a wave runs either the doubling (7 Fq-mul) or the addition (16 "
+                                       "Fq-mul: the bases sit in LDS, their z^2, z^3 are recomputed) for one chain "
+                                       "of each lane whose chain waits for it -- 1.30x the chains' own weight "
+                                       "(profiles/r4c_g1mul2_schedule_counters.json; one chain per lane: 1.41x)"}
         m = min(args.cpu_sample or 2048, n)
+        # rows of both chains of the first lanes: i and i + ceil(n / 2)
+        h = (n + 1) // 2
+        rows = np.unique(np.r_[np.arange(min(m // 2, h)), h + np.arange(min(m - m // 2, n - h))])
         threads = host_cpus()["usable"]
-        ph, kh, oh = (t[:m].cpu().numpy().view(np.uint64) for t in (P, k2, out))
+        ridx = torch.from_numpy(rows).to(dev)
+        ph, kh, oh = (t[ridx].cpu().numpy().view(np.uint64) for t in (P, k2, out))
         t0 = time.perf_counter()
         ref = O.g1_mul(ph, kh, threads)
         dt = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": m / dt, "unit": unit, "cores": threads, "kind": "port",
-                               "sample": "%d G1*Fr of the bench inputs, oracle, %d threads" % (m, threads),
+        res["cpu_baseline"] = {"value": len(rows) / dt, "unit": unit, "cores": threads, "kind": "port",
+                               "sample": "%d G1*Fr of the bench inputs (rows 0.. and n/2.., both chains of the "
+                                         "first lanes), oracle, %d threads" % (len(rows), threads),
                                "parity_sample_bit_exact": bool(np.array_equal(ref, oh))}
     print(json.dumps(res), flush=True)
 

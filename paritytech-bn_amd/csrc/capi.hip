@@ -538,11 +538,16 @@ int clear_err(bn_ctx* c, hipStream_t s) {
     RET_IF(ws_acquire((ctx), (ctx)->stream)); \
     WsUse ws_use_{(ctx), (ctx)->stream}
 
-// k_g1_mul: kPairBlock-thread blocks (two waves on every SIMD, kernels.h issue
-// balance) once the batch gives every CU one such block, else kBlock
+// k_g1_mul2 (two chains per lane) once half the batch gives every CU one
+// kPairBlock-thread block: 8.82 -> 8.36 ms at config 3's 2^18
+// (profiles/r4c_ab_g1mul2.txt); below that k_g1_mul, one chain per lane, in
+// kPairBlock-thread blocks (two waves on every SIMD, kernels.h issue balance)
+// once the batch gives every CU one such block, else kBlock
 constexpr size_t kG1MulPairBlockMin = (size_t)256 * kPairBlock;
 static void g1_mul_launch(const bn_g1* d_p, const bn_fr* d_k, size_t n, bn_g1* d_out, hipStream_t s) {
-    if (n >= kG1MulPairBlockMin)
+    if ((n + 1) / 2 >= kG1MulPairBlockMin)
+        k_g1_mul2<<<grid_pair((n + 1) / 2), kPairBlock, 0, s>>>(d_p, d_k, n, d_out);
+    else if (n >= kG1MulPairBlockMin)
         k_g1_mul<<<grid_pair(n), kPairBlock, 0, s>>>(d_p, d_k, n, d_out);
     else
         k_g1_mul<<<grid_for(n), kBlock, 0, s>>>(d_p, d_k, n, d_out);

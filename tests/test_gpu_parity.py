@@ -240,6 +240,27 @@ def test_config3_g1_mul_full_size(ctx):
     assert np.array_equal(got, O.g1_mul(base, S, NT))
 
 
+def test_g1_mul_two_chain_odd_tail(ctx):
+    """The two-chains-per-lane kernel (k_g1_mul2, lane i runs rows i and i + h,
+    h = ceil(n / 2)) at an odd size: the last lane has one chain.  Zero bases, zero
+    scalars, k = 1 and k = r - 1 planted in both halves; rows around 0, h and the
+    tail checked against the oracle."""
+    n = (1 << 18) + 3
+    h = (n + 1) // 2
+    _, S = O.random_scalars(n, seed=444, lo=0)
+    base = ctx.g1_mul_many(np.tile(O.g1_one(), (n, 1)), np.roll(S, 11, axis=0))
+    one = O.canon_to_mont_array([1]).reshape(4)
+    for row in (1, h + 1, n - 1):
+        base[row] = 0
+        base[row, 4:8] = one                          # G1::zero()
+    S[[2, h + 2, n - 2]] = 0
+    S[[3, h + 3]] = O.canon_to_mont_array([1], O.FR).reshape(4)
+    S[[4, h + 4]] = O.canon_to_mont_array([O.R - 1], O.FR).reshape(4)
+    got = ctx.g1_mul_many(base, S)
+    rows = np.r_[0:64, h - 64:h + 64, n - 64:n]
+    assert np.array_equal(got[rows], O.g1_mul(base[rows], S[rows], NT))
+
+
 # ---- the throughput path (the kernels `value` measures) on the edge cases, vs the oracle
 def test_throughput_path_pairing_many(ctx_tp, pairs):
     p, q = pairs

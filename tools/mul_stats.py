@@ -49,18 +49,24 @@ def main():
     ctx.dev_status()
     fn(st.ctypes.data)
     adds, dbls, lane_adds, lane_dbls, live = (int(x) for x in st)
-    waves = (n + 63) // 64
-    weight_wave = (14 * adds + 7 * dbls) / waves
+    # k_g1_mul2 (two chains per lane, capi.hip g1_mul_launch) from 2^18 rows on;
+    # its addition recomputes the base's z^2, z^3 (16 Fq-mul, the bases sit in LDS)
+    chains = 2 if (n + 1) // 2 >= 256 * 512 else 1
+    add_w = 16 if chains == 2 else 14
+    waves = ((n + chains - 1) // chains + 63) // 64
+    weight_wave = (add_w * adds + 7 * dbls) / waves
     weight_lane = (14 * lane_adds + 7 * lane_dbls) / n
     print(json.dumps({
         "n": n, "waves": waves, "add_iterations_per_wave": adds / waves, "dbl_iterations_per_wave": dbls / waves,
         "adds_per_lane": lane_adds / n, "dbls_per_lane": lane_dbls / n,
         "fqmul_weight_per_wave": weight_wave, "fqmul_weight_per_lane_needed": weight_lane,
-        "schedule_overhead": weight_wave / weight_lane,
+        "chains_per_lane": chains, "addition_weight": add_w,
+        "schedule_overhead": weight_wave / (chains * weight_lane),
         "occupancy_of_iterations": (lane_adds + lane_dbls) / (64.0 * (adds + dbls)),
         "occupancy_of_unfinished_lanes": (lane_adds + lane_dbls) / max(live, 1),
-        "what": "ballot schedule of curve.h jac_mul on config 3's launch: per wave the additions (14 Fq-mul) and "
-                "doublings (7) run, against the weight each lane's own chain needs"}), flush=True)
+        "what": "ballot schedule of curve.h jac_mul / jac_mul2 on config 3's launch: per wave the additions "
+                "(addition_weight Fq-mul) and doublings (7) run, against the weight the wave's chains need "
+                "(their additions at 14, the base's z^2, z^3 computed once)"}), flush=True)
 
 
 if __name__ == "__main__":
