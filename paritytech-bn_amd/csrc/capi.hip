@@ -314,29 +314,39 @@ uint32_t* slot_region(bn_ctx* c, int k) { return c->slots + (size_t)k * kSlotWor
 constexpr int kRegionA = 1, kRegionB = 2;  // ping-pong regions of the product reduction
 constexpr int kRegionParts = 3;            // per-chunk partial products
 constexpr int kRegionResult = 4;           // the final product (element 0, stride 1)
-constexpr size_t kWideElemsPerBlock = 2 * (kBlock / 16);  // k_fq12_reduce_wide: 32 elements per block
+constexpr size_t kWideGroups = kBlock / 16;  // k_fq12_reduce_wide: 16-lane groups per block
+constexpr size_t kReduceBlocksMax = 512;      // two rounds of 256-thread blocks (one per CU: 248 + 32 registers)
 
 // Multiply each of `sets` sets of n split-layout values together on the wide
-// layout (k_fq12_reduce_wide, a factor of 32 per launch, all sets in one
-// launch): set y is elements y * in_set + [0, n) of `in` (stride in_stride),
-// its product goes to element out_base + y * out_set of `out` (stride
-// out_stride).  `in` must not be a ping-pong region.
+// layout (k_fq12_reduce_wide, all sets in one launch per level): set y is
+// elements y * in_set + [0, n) of `in` (stride in_stride), its product goes to
+// element out_base + y * out_set of `out` (stride out_stride).  `in` must not
+// be a ping-pong region.  Each level's chain length per group G is the smallest
+// power of two >= 2 that needs at most two rounds of blocks on the CUs: config
+// 5's 16 x 4,096 segment values take two launches (G = 8, then 2) instead of
+// three of G = 2 -- 2.20 against 2.25-2.26 ms per product; one round (G = 16)
+// 2.21-2.27, G = 32 2.27-2.30 (profiles/r4e_ab_reduce.txt).
 int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, size_t n, size_t in_set, int sets, uint32_t* out,
                  size_t out_stride, size_t out_base, size_t out_set, hipStream_t s) {
     const uint32_t* src = in;
     size_t sn = n, sstride = in_stride, sset = in_set;
     bool a = true;
     for (;;) {
-        const size_t blocks = (sn + kWideElemsPerBlock - 1) / kWideElemsPerBlock;
+        int per_group = 2;
+        while (per_group < 64 && (size_t)sets * ((sn + kWideGroups * per_group - 1) / (kWideGroups * per_group)) >
+                                     kReduceBlocksMax)
+            per_group *= 2;
+        const size_t per_block = kWideGroups * (size_t)per_group;
+        const size_t blocks = (sn + per_block - 1) / per_block;
         if (blocks == 1) {
             k_fq12_reduce_wide<<<dim3(1, sets), kBlock, 0, s>>>(src, sstride, sn, sset, out, out_stride, out_base,
-                                                                out_set);
+                                                                out_set, per_group);
             HIPCHK(c, hipGetLastError());
             return BN_OK;
         }
         uint32_t* dst = slot_region(c, a ? kRegionA : kRegionB);
         k_fq12_reduce_wide<<<dim3((unsigned)blocks, sets), kBlock, 0, s>>>(src, sstride, sn, sset, dst,
-                                                                            sets * blocks, 0, blocks);
+                                                                            sets * blocks, 0, blocks, per_group);
         HIPCHK(c, hipGetLastError());
         src = dst;
         sstride = sets * blocks;

@@ -139,8 +139,11 @@ BN_INLINE Jac<F> jac_add_pre(const Jac<F>& s, const Jac<F>& o, bool o_zero, cons
     auto s2 = F_mul(o.y, z1_cubed);
     auto h = F_sub(u2, u1);
     auto s2_minus_s1 = F_sub(s2, s1);
-    // u1 == u2 && s1 == s2  <=>  h == 0 && s2 - s1 == 0 (mod p)
-    const bool same = F_is_zero(h) && F_is_zero(s2_minus_s1);
+    // u1 == u2 && s1 == s2  <=>  h == 0 && s2 - s1 == 0 (mod p); the second test only
+    // when some lane of the wave has h == 0 (rare: wave-uniform guard)
+    const bool h_zero = F_is_zero(h);
+    bool same = false;
+    if (BN_ANY(h_zero)) same = h_zero && F_is_zero(s2_minus_s1);
     auto i = F_sqr(F_add(h, h));
     auto j = F_mul(h, i);
     auto r = F_add(s2_minus_s1, s2_minus_s1);
@@ -315,13 +318,33 @@ BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8], Step&& step = Ste
 // two).  Each chain's own steps keep their order: both outputs stay bit-exact.
 // `base(c)` returns the base of chain c (0/1); the kernel keeps the two bases in
 // LDS, so the loop holds two accumulators in registers, not four points.
-template <template <int> class F, typename Base, typename Step = NoBitStep>
-BN_INLINE void jac_mul2(Base&& base, bool z0, bool z1, const uint32_t k0[8], const uint32_t k1[8], Jac<F>& out0,
-                        Jac<F>& out1, Step&& step = Step{}) {
+// `bit(c, i)` returns bit i of chain c's canonical scalar and `top0`/`top1` are the
+// scalars' top set bits (-1 for zero): the kernel keeps the scalars in LDS too, so
+// a doubling reads the one bit it consumes instead of shifting 256-bit registers.
+struct ChainPos {
+    int left;       // bits below the current one still to consume
+    bool need_add;  // the next step is the addition of the current bit
+    BN_INLINE void init(int top) {
+        need_add = top >= 0;  // zero + p: the reference's first addition (found_one)
+        left = top;
+    }
+    BN_INLINE bool wants_dbl() const { return !need_add && left > 0; }
+};
+// the top set bit of a 256-bit scalar, -1 for zero
+BN_INLINE int scalar_top_bit(const uint32_t k[8]) {
+    int top = -1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (k[i]) top = 32 * i + 31 - __builtin_clz(k[i]);
+    return top;
+}
+template <template <int> class F, typename Base, typename Bit, typename Step = NoBitStep>
+BN_INLINE void jac_mul2(Base&& base, Bit&& bit, bool z0, bool z1, int top0, int top1, Jac<F>& out0, Jac<F>& out1,
+                        Step&& step = Step{}) {
     Jac<F> r0 = jac_zero<F>(), r1 = jac_zero<F>();
-    MulBits m0, m1;
-    m0.init(k0);
-    m1.init(k1);
+    ChainPos m0, m1;
+    m0.init(top0);
+    m1.init(top1);
     int it = 0;
 #pragma unroll 1
     for (;;) {
@@ -349,11 +372,17 @@ BN_INLINE void jac_mul2(Base&& base, bool z0, bool z1, const uint32_t k0[8], con
         r0 = {F_select(w0, t.x, r0.x), F_select(w0, t.y, r0.y), F_select(w0, t.z, r0.z)};
         r1 = {F_select(w1, t.x, r1.x), F_select(w1, t.y, r1.y), F_select(w1, t.z, r1.z)};
         if (do_add) {
-            m0.added(w0);
-            m1.added(w1);
+            m0.need_add = w0 ? false : m0.need_add;
+            m1.need_add = w1 ? false : m1.need_add;
         } else {
-            m0.doubled(w0);
-            m1.doubled(w1);
+            // the doubling consumed bit left - 1 of the chain that ran: its addition is
+            // pending when the bit is set
+            const int pos = (use0 ? m0.left : m1.left) - 1;
+            const bool b = bit(use0 ? 0 : 1, pos < 0 ? 0 : pos);
+            m0.need_add = w0 ? b : m0.need_add;
+            m1.need_add = w1 ? b : m1.need_add;
+            m0.left -= w0 ? 1 : 0;
+            m1.left -= w1 ? 1 : 0;
         }
     }
     out0 = r0;

@@ -544,7 +544,7 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
                                                     int* __restrict__ err, int duo);
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
                                                              size_t n, size_t in_set, uint32_t* __restrict__ out,
-                                                             size_t out_stride, size_t out_base, size_t out_set);
+                                                             size_t out_stride, size_t out_base, size_t out_set, int per_group);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
 // (a producer wave for the lines, consumer groups for the wide Miller loop + FE)
 constexpr int kLatPairs = 8;

@@ -30,12 +30,14 @@ __global__ void __launch_bounds__(kPairBlock) k_g1_mul(const bn_g1* __restrict__
 }
 // Two chains per lane (curve.h jac_mul2): lane i multiplies elements i and i + h,
 // h = ceil(n / 2); the odd tail's second chain has the zero scalar.  The two bases
-// sit in LDS, word-major ([word][thread], conflict-free): 2 x 27 words per thread,
-// 110.6 KB per 512-thread block besides the fold table.
+// and the two canonical scalars sit in LDS, word-major ([word][thread],
+// conflict-free): 2 x (27 + 8) words per thread, 143 KB per 512-thread block
+// besides the fold table.
 constexpr int kMul2Words = 27;
+constexpr int kMul2Slots = 2 * kMul2Words + 16;
 __global__ void __launch_bounds__(kPairBlock) k_g1_mul2(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k,
                                                       size_t n, bn_g1* __restrict__ out) {
-    __shared__ uint32_t bases[2 * kMul2Words][kPairBlock];
+    __shared__ uint32_t lds[kMul2Slots][kPairBlock];
     fold_table_init();
     const Balance bal = balance_init();
     const size_t h = (n + 1) / 2;
@@ -45,25 +47,33 @@ __global__ void __launch_bounds__(kPairBlock) k_g1_mul2(const bn_g1* __restrict_
     const size_t j = i + h;
     const bool has1 = j < n;
     const size_t j1 = has1 ? j : i;
-    uint32_t s0[8], s1[8];
-    fr_to_canonical(k[i], s0);
-    fr_to_canonical(k[j1], s1);
-#pragma unroll
-    for (int t = 0; t < 8; ++t) s1[t] = has1 ? s1[t] : 0u;
     bool z0, z1;
+    int top0, top1;
     {
+        uint32_t s0[8], s1[8];
+        fr_to_canonical(k[i], s0);
+        fr_to_canonical(k[j1], s1);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) s1[t] = has1 ? s1[t] : 0u;
+        top0 = scalar_top_bit(s0);
+        top1 = scalar_top_bit(s1);
         const G1J a0 = {widen<kPt>(ld_ref(p[i].x)), widen<kPt>(ld_ref(p[i].y)), widen<kPt>(ld_ref(p[i].z))};
         const G1J a1 = {widen<kPt>(ld_ref(p[j1].x)), widen<kPt>(ld_ref(p[j1].y)), widen<kPt>(ld_ref(p[j1].z))};
         z0 = jac_is_zero(a0);
         z1 = jac_is_zero(a1);
 #pragma unroll
         for (int w = 0; w < 9; ++w) {
-            bases[w][tid] = a0.x.v[w];
-            bases[9 + w][tid] = a0.y.v[w];
-            bases[18 + w][tid] = a0.z.v[w];
-            bases[kMul2Words + w][tid] = a1.x.v[w];
-            bases[kMul2Words + 9 + w][tid] = a1.y.v[w];
-            bases[kMul2Words + 18 + w][tid] = a1.z.v[w];
+            lds[w][tid] = a0.x.v[w];
+            lds[9 + w][tid] = a0.y.v[w];
+            lds[18 + w][tid] = a0.z.v[w];
+            lds[kMul2Words + w][tid] = a1.x.v[w];
+            lds[kMul2Words + 9 + w][tid] = a1.y.v[w];
+            lds[kMul2Words + 18 + w][tid] = a1.z.v[w];
+        }
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            lds[2 * kMul2Words + w][tid] = s0[w];
+            lds[2 * kMul2Words + 8 + w][tid] = s1[w];
         }
     }
     // each thread reads only its own column: no barrier needed
@@ -72,14 +82,15 @@ __global__ void __launch_bounds__(kPairBlock) k_g1_mul2(const bn_g1* __restrict_
         const int o = c * kMul2Words;
 #pragma unroll
         for (int w = 0; w < 9; ++w) {
-            b.x.v[w] = bases[o + w][tid];
-            b.y.v[w] = bases[o + 9 + w][tid];
-            b.z.v[w] = bases[o + 18 + w][tid];
+            b.x.v[w] = lds[o + w][tid];
+            b.y.v[w] = lds[o + 9 + w][tid];
+            b.z.v[w] = lds[o + 18 + w][tid];
         }
         return b;
     };
+    auto bit = [&](int c, int pos) { return ((lds[2 * kMul2Words + 8 * c + (pos >> 5)][tid] >> (pos & 31)) & 1u) != 0; };
     G1J r0, r1;
-    jac_mul2<Fq>(base, z0, z1, s0, s1, r0, r1, [&](int t) { balance_step(bal, (uint32_t)t); });
+    jac_mul2<Fq>(base, bit, z0, z1, top0, top1, r0, r1, [&](int t) { balance_step(bal, (uint32_t)t); });
     st_ref(out[i].x, r0.x);
     st_ref(out[i].y, r0.y);
     st_ref(out[i].z, r0.z);

@@ -117,8 +117,8 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
 
 // Product reduction of several independent sets (blockIdx.y = set y, the
 // elements y * in_set + [0, n) of `in`, split layout, stride in_stride): block
-// (b, y) multiplies the set's elements [32b, 32b + 32) -- one product per group
-// of the two elements 2g, 2g + 1, then a tree over the 16 groups through LDS --
+// (b, y) multiplies the set's elements [16Gb, 16Gb + 16G) (G = per_group) -- a
+// chain of G factors per group, then a tree over the 16 groups through LDS --
 // and writes the block's product as element out_base + y * out_set + b of `out`
 // (stride out_stride).  Elements past n count as one.  The order of the factors
 // differs from the reference's left-to-right accumulation; Fq12 multiplication
@@ -127,24 +127,33 @@ __shared__ uint32_t g_wval[kWGroups * kWLanes * kWSlot];  // 12 KB: one value pe
 
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
                                                              size_t n, size_t in_set, uint32_t* __restrict__ out,
-                                                             size_t out_stride, size_t out_base, size_t out_set) {
+                                                             size_t out_stride, size_t out_base, size_t out_set,
+                                                             int per_group) {
     fold_table_init();
     const WL w = wl();
     const int g = (int)threadIdx.x / kWLanes;
-    const size_t base = (size_t)blockIdx.x * 2 * kWGroups;
-    const size_t e0 = base + 2 * g, e1 = e0 + 1, sb = (size_t)blockIdx.y * in_set;
+    // group g multiplies elements [e0, e0 + per_group) of its block's range in a
+    // chain (the next factor's load issued before the product that precedes it;
+    // factors past n are one), then the groups' values meet in the tree below
+    const size_t e0 = ((size_t)blockIdx.x * kWGroups + g) * (size_t)per_group, sb = (size_t)blockIdx.y * in_set;
     const Fq<2> one = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
-    const Fq<2> a = e0 < n ? w_ld_split(in, in_stride, sb + e0, w) : one;
-    const Fq<2> b = e1 < n ? w_ld_split(in, in_stride, sb + e1, w) : one;
-    Fq<2> x = e1 < n ? w12_mul(a, b) : a;  // uniform per group
+    Fq<2> x = e0 < n ? w_ld_split(in, in_stride, sb + e0, w) : one;
+    Fq<2> y = e0 + 1 < n ? w_ld_split(in, in_stride, sb + e0 + 1, w) : one;
+#pragma unroll 1
+    for (int t = 1; t < per_group; ++t) {
+        const size_t e = e0 + t + 1;
+        const Fq<2> y_next = (t + 1 < per_group && e < n) ? w_ld_split(in, in_stride, sb + e, w) : one;
+        if (e0 + t < n) x = w12_mul(x, y);  // uniform per group
+        y = y_next;
+    }
     uint32_t* mine = g_wval + (g * kWLanes) * kWSlot;
 #pragma unroll 1
     for (int s = kWGroups / 2; s >= 1; s /= 2) {
         w_put(mine, w.l, x);
         __syncthreads();
         if (g < s) {
-            const Fq<2> y = w_get<2>(g_wval + ((g + s) * kWLanes) * kWSlot, w.l);
-            x = w12_mul(x, y);
+            const Fq<2> y2 = w_get<2>(g_wval + ((g + s) * kWLanes) * kWSlot, w.l);
+            x = w12_mul(x, y2);
         }
         __syncthreads();
     }

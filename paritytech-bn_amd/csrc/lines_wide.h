@@ -92,10 +92,13 @@ __device__ __forceinline__ Fq2<B> pw_from(const Fq2<B>& x, int j) {
     for (int d = 0; d < 9; ++d) r.c.v[d] = (uint32_t)__shfl((int)x.c.v[d], src);
     return r;
 }
+// slot k's operand as a tree on the bits of k: where the four are two pairs of the
+// same value (a0 == a2, a1 == a3) the compiler merges the outer select away
 template <int B>
 __device__ __forceinline__ Fq2<B> pw_pick(int k, const Fq2<B>& a0, const Fq2<B>& a1, const Fq2<B>& a2,
                                           const Fq2<B>& a3) {
-    return fq2_select(k == 0, a0, fq2_select(k == 1, a1, fq2_select(k == 2, a2, a3)));
+    const bool b0 = (k & 1) != 0, b1 = (k & 2) != 0;
+    return fq2_select(b1, fq2_select(b0, a3, a2), fq2_select(b0, a1, a0));
 }
 template <class T>
 struct Fq2K;

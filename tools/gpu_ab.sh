@@ -1,24 +1,17 @@
 #!/bin/bash
-# A/B of library variants exp/lib_<V>.so on config 2 (HBM-resident 2^16 pairs,
-# per-kernel HIP-event times), ROUNDS interleaved rounds.  Optional WORKLOADS
-# (space-separated bench.py --workload names) run after each config-2 line.
-# Usage: tools/gpu_ab.sh OUTDIR ROUNDS V1 V2 ...
-OUT=$1; ROUNDS=$2; shift 2
+# Interleaved A/B of two library builds on configs 3 and 5 (and optionally config 2):
+#   tools/gpu_ab.sh TAG LIB_A LIB_B [workloads]   (LIB_* = path of a libbn254mi.so build)
+set -e
+TAG=$1; A=$2; B=$3; W=${4:-"g1mul product"}
+OUT=gpurun_out/$TAG
 mkdir -p $OUT
-for r in $(seq 1 $ROUNDS); do for v in "$@"; do
-  BN254MI_LIB=exp/lib_$v.so timeout -k 5 150 python -u bench.py --no-cpu-baseline --no-e2e --steps 20 \
-    > $OUT/$v$r.json 2> $OUT/$v$r.err || { echo "bench failed: $v$r"; tail -5 $OUT/$v$r.err; exit 1; }
-  for w in $WORKLOADS; do
-    BN254MI_LIB=exp/lib_$v.so timeout -k 5 150 python -u bench.py --workload $w --steps 10 --cpu-sample 64 \
-      > $OUT/${v}${r}_$w.json 2>> $OUT/$v$r.err || { echo "bench $w failed: $v$r"; exit 1; }
+for r in 1 2; do
+  for w in $W; do
+    for L in A B; do
+      lib=$A; [ $L = B ] && lib=$B
+      if [ $w = pairing ]; then args=""; else args="--workload $w"; fi
+      BN254MI_LIB=$lib timeout -k 10 120 python -u bench.py $args --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --no-config4-ref > $OUT/${w}_${L}_$r.json 2> $OUT/${w}_${L}_$r.err
+      python3 -c "import json; d=json.load(open('$OUT/${w}_${L}_$r.json')); print('$w $L r$r', round(d['ms_per_step'],4))"
+    done
   done
-  python3 - <<PY
-import json, os
-d = json.load(open("$OUT/$v$r.json"))
-extra = ""
-for w in "$WORKLOADS".split():
-    x = json.load(open("$OUT/${v}${r}_%s.json" % w))
-    extra += " %s %.3f ms" % (w, x.get("roofline", {}).get("per_step_ms") or x.get("kernel", {}).get("per_launch_ms") or x["ms_per_step"])
-print("$v$r", round(d["value"]), d["roofline"]["per_launch_ms"], extra, flush=True)
-PY
-done; done
+done
