@@ -118,7 +118,8 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
 // Product reduction of several independent sets (blockIdx.y = set y, the
 // elements y * in_set + [0, n) of `in`, split layout, stride in_stride): block
 // (b, y) multiplies the set's elements [16Gb, 16Gb + 16G) (G = per_group) -- a
-// chain of G factors per group, then a tree over the 16 groups through LDS --
+// chain of G factors per group (elements g, g + 16, ...), then a tree over the 16
+// groups through LDS --
 // and writes the block's product as element out_base + y * out_set + b of `out`
 // (stride out_stride).  Elements past n count as one.  The order of the factors
 // differs from the reference's left-to-right accumulation; Fq12 multiplication
@@ -132,18 +133,19 @@ __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __r
     fold_table_init();
     const WL w = wl();
     const int g = (int)threadIdx.x / kWLanes;
-    // group g multiplies elements [e0, e0 + per_group) of its block's range in a
-    // chain (the next factor's load issued before the product that precedes it;
-    // factors past n are one), then the groups' values meet in the tree below
-    const size_t e0 = ((size_t)blockIdx.x * kWGroups + g) * (size_t)per_group, sb = (size_t)blockIdx.y * in_set;
+    // group g multiplies elements e0 + 16t (t < per_group) of its block's range in
+    // a chain -- at each step the block's 16 groups read 16 consecutive elements --
+    // with the next factor's load issued before the product that precedes it
+    // (factors past n are skipped), then the groups' values meet in the tree below
+    const size_t e0 = (size_t)blockIdx.x * kWGroups * (size_t)per_group + g, sb = (size_t)blockIdx.y * in_set;
     const Fq<2> one = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
     Fq<2> x = e0 < n ? w_ld_split(in, in_stride, sb + e0, w) : one;
-    Fq<2> y = e0 + 1 < n ? w_ld_split(in, in_stride, sb + e0 + 1, w) : one;
+    Fq<2> y = e0 + kWGroups < n ? w_ld_split(in, in_stride, sb + e0 + kWGroups, w) : one;
 #pragma unroll 1
     for (int t = 1; t < per_group; ++t) {
-        const size_t e = e0 + t + 1;
+        const size_t e = e0 + (size_t)(t + 1) * kWGroups;
         const Fq<2> y_next = (t + 1 < per_group && e < n) ? w_ld_split(in, in_stride, sb + e, w) : one;
-        if (e0 + t < n) x = w12_mul(x, y);  // uniform per group
+        if (e0 + (size_t)t * kWGroups < n) x = w12_mul(x, y);  // uniform per group
         y = y_next;
     }
     uint32_t* mine = g_wval + (g * kWLanes) * kWSlot;

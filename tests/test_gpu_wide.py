@@ -129,6 +129,18 @@ def test_config5_product_2_14(ctx):
     assert np.array_equal(out.cpu().numpy().view(np.uint64), O.pairing_batch(p, q, nthreads=NT))
 
 
+def test_product_ragged_reduction_chains(ctx):
+    """A 12,345-term pairing_batch and miller_loop_batch: K = 2 pairs per lane pair,
+    6,173 segment values per set, so the first reduction level runs chains of
+    G = 16 factors per group with a ragged last block (capi.hip product_wide), the
+    second a single block; bit-exact against the oracle."""
+    n = 12345
+    p, q, _, _ = O.random_pairs(n, seed=12345, nthreads=NT)
+    assert np.array_equal(ctx.pairing_batch(p, q), O.pairing_batch(p, q, nthreads=NT))
+    rc, want = O.miller_loop_batch(q[:4099], p[:4099])
+    assert rc == 0 and np.array_equal(ctx.miller_loop_batch(q[:4099], p[:4099]), want)
+
+
 def test_product_across_chunks_is_one(ctx):
     """2^18 + 2 terms (two chunks of the reduction): pairs (s_i G1, t_i G2) and
     ((r - s_i) G1, t_i G2), so the product is e(G1, G2)^(r t) = Gt::one() --
