@@ -279,7 +279,7 @@ def other_workload(args, local_rank):
                            "traffic_source": "profiles/pmc_summary.json product_step: FETCH_SIZE (read-factor "
                                              "corrected) + WRITE_SIZE of every kernel of one product, committed "
                                              "rocprofv3 PMC passes, not measured in this run",
-                           "kernel": "whole product (k_prepare_wide, k_miller_seg, k_fq12_reduce_wide x3, "
+                           "kernel": "whole product (k_prepare_wide, k_miller_seg, k_fq12_reduce_wide x2, "
                                      "k_horner_tree)",
                            "per_step_ms": ms,
                            "basis": "SURVEY.md 8(d) config 5: n*(19+2655+3741) + 2304 + 8767 Fq-mul, x128 MAD32"}
