@@ -74,30 +74,50 @@ void he_fq12_frob(const uint32_t* a, int power, uint32_t* o) {
 void he_fq12_mul_by_024(const uint32_t* f, const uint32_t* e0, const uint32_t* evw, const uint32_t* evv, uint32_t* o) {
     st12(fq12_mul_by_024(ld12(f), ld2(e0), ld2(evw), ld2(evv)), o);
 }
-// k_gt_pow's formulas (kernels_gtpow.hip): 4-bit window table x^0..x^15, then
-// 63 windows of four squarings and one product; e = canonical scalar words.  The
-// squarings are cyclotomic when x is a nonzero cyclotomic-subgroup member
-// (x^(p^4) * x == x^(p^2)), as for a whole wave of such elements on the device.
-// Returns 1 when the cyclotomic chain ran.
+// k_gt_pow's formulas (kernels_gtpow.hip): when x is a nonzero cyclotomic-subgroup
+// member (x^(p^4) * x == x^(p^2)), as for a whole wave of such elements on the
+// device, signed 5-bit windows (Booth digits -16..16 from bits 5i - 1 .. 5i + 4,
+// negative digits by the conjugate) over a table x^0..x^16 with cyclotomic
+// squarings; otherwise unsigned 4-bit windows over x^0..x^15 with generic
+// squarings.  e = canonical scalar words.  Returns 1 when the cyclotomic chain ran.
 int he_gt_pow(const uint32_t* a, const uint32_t* e_in, uint32_t* o) {
-    Fq12<kF> tab[16];
+    Fq12<kF> tab[17];
     tab[0] = widen<kF>(fq12_one());
     tab[1] = widen<kF>(ld12(a));
-    for (int j = 2; j < 16; ++j) tab[j] = mul12(tab[j - 1], tab[1]);
+    for (int j = 2; j < 17; ++j) tab[j] = mul12(tab[j - 1], tab[1]);
     const Fq12<kF> x2 = narrow12<kF>(fq12_frobenius_map<2>(tab[1]));
     const Fq12<kF> x4x = mul12(narrow12<kF>(fq12_frobenius_map<2>(x2)), tab[1]);
     const bool cyc = fq12_is_zero(fq12_sub(x4x, x2)) && !fq12_is_zero(tab[1]);
     uint32_t e[8];
     memcpy(e, e_in, sizeof e);
+    if (cyc) {
+        for (int s = 7; s > 0; --s) e[s] = (e[s] << 1) | (e[s - 1] >> 31);
+        e[0] <<= 1;
+        auto entry = [&](uint32_t f) {
+            const uint32_t v = (f >> 1) + (f & 1u);
+            const bool neg = (f & 32u) != 0 && v != 32u;
+            const uint32_t mag = (f & 32u) ? 32u - v : v;
+            return neg ? Fq12<kF>(fq12_conj(tab[mag])) : tab[mag];
+        };
+        Fq12<kF> acc = entry(e[7] >> 26);
+        for (int w = 49; w >= 0; --w) {
+            for (int s = 7; s > 0; --s) e[s] = (e[s] << 5) | (e[s - 1] >> 27);
+            e[0] <<= 5;
+            for (int s = 0; s < 5; ++s) acc = cyc_sqr(acc);
+            acc = mul12(acc, entry(e[7] >> 26));
+        }
+        st12(acc, o);
+        return 1;
+    }
     Fq12<kF> acc = tab[e[7] >> 28];
     for (int w = 62; w >= 0; --w) {
         for (int s = 7; s > 0; --s) e[s] = (e[s] << 4) | (e[s - 1] >> 28);
         e[0] <<= 4;
-        for (int s = 0; s < 4; ++s) acc = cyc ? cyc_sqr(acc) : narrow12<kF>(fq12_sqr(acc));
+        for (int s = 0; s < 4; ++s) acc = narrow12<kF>(fq12_sqr(acc));
         acc = mul12(acc, tab[e[7] >> 28]);
     }
     st12(acc, o);
-    return cyc;
+    return 0;
 }
 void he_final_exp(const uint32_t* f, uint32_t* o) {
     st12(fe_last_chunk(fe_first_chunk(widen<kF>(ld12(f)))), o);

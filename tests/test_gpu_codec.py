@@ -142,6 +142,9 @@ def test_gt_pow(ctx):
     k[0] = O.canon_to_mont_array([0], O.FR)
     k[1] = O.canon_to_mont_array([1], O.FR)
     k[2] = O.canon_to_mont_array([R - 1], O.FR)
+    # runs of ones and alternating bits (the signed 5-bit windows' carries and +-16 digits)
+    k[3:7] = O.canon_to_mont_array([(1 << 250) - 1, (1 << 253) - 1, int("01" * 126, 2), int("10000" * 50, 2)],
+                                   O.FR).reshape(4, 4)
     out = ctx.gt_pow_many(a, k)
     assert np.array_equal(out, O.gt_pow(a, k))
     # waves holding only pairing outputs take the cyclotomic squarings, the rest the

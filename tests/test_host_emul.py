@@ -93,7 +93,8 @@ def test_gt_pow_formulas():
     p, q, _, _ = O.random_pairs(2, seed=61)
     a = np.concatenate([O.pairing_many(p[:1], q[:1]), O.miller_loop_batch(q[1:2], p[1:2])[1][None]])
     vals, k = O.random_scalars(2, 62, lo=0)
-    for scal in (vals[0], 0, 1, O.R - 1):
+    # with runs of ones and alternating bits: Booth digits 0 with a carry (six ones), -1, +-16
+    for scal in (vals[0], 0, 1, O.R - 1, (1 << 250) - 1, (1 << 253) - 1, int("01" * 126, 2), int("10000" * 50, 2)):
         K = O.canon_to_mont_array([scal], O.FR).reshape(1, 4)
         words = np.frombuffer(int(scal).to_bytes(32, "little"), np.uint64).copy()
         for j in range(2):
