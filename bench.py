@@ -25,7 +25,7 @@ The points come from the engine's own scalar-multiplication kernels, kept in
 Jacobian form (z != 1) -- exactly the reference's `G * Fr` output images.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4]
-    python bench.py --workload g1mul|product|g2validate|g2decompress|gtpow
+    python bench.py --workload g1mul|g2mul|product|g2validate|g2decompress|gtpow
     python bench.py --gpus 2 --dry-run-cpu   # control flow on CPU (gloo, stub engine)
 """
 import argparse
@@ -230,7 +230,17 @@ def other_workload(args, local_rank):
     sh = stream.cuda_stream
     res = {"n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "u32 (9x29-bit Montgomery digits, integer only)", "data": "synthetic"}
-    if args.workload == "g1mul":
+    if args.workload == "g2mul":
+        n = args.pairs
+        _, Qb = device_points(ctx, n, None, 7, dev, sh)  # random Jacobian G2 bases
+        k2 = torch.from_numpy(fr_images(n, 8).view(np.int64)).to(dev)
+        P = Qb
+        out = torch.empty_like(Qb)
+        step = lambda: ctx.g2_mul_many_dev(Qb.data_ptr(), k2.data_ptr(), n, out.data_ptr(), sh)  # noqa: E731
+        unit = "G2 scalar muls/s"
+        res["config"] = {"workload": "SURVEY 8(f1): batched Fr x G2 (reference double-and-add chain, bit-exact "
+                                     "Jacobian output)", "muls": n}
+    elif args.workload == "g1mul":
         n = args.pairs if args.pairs != (1 << 16) else (1 << 18)
         P, _ = device_points(ctx, n, 5, None, dev, sh)  # random Jacobian bases
         k2 = torch.from_numpy(fr_images(n, 6).view(np.int64)).to(dev)
@@ -299,6 +309,25 @@ def other_workload(args, local_rank):
                                          "threads (orc_pairing_batch_mt), %.2f s wall" % (threads, dt),
                                "parity_bit_exact": bool(np.array_equal(ref, gout.cpu().numpy().view(np.uint64))
                                                         and int(gst.item()) == 0)}
+    elif args.workload == "g2mul":
+        # ~9,165 Fq-mul per 254-bit G2 scalar multiplication, x128 MAD32
+        ms = e0.elapsed_time(e1) / args.steps
+        work = n * 9165 * MAD32_PER_FQMUL
+        res["roofline"] = {"bound": "valu", "achieved": work / (ms * 1e-3) / 1e12, "peak": PEAK_MAD32_PER_S / 1e12,
+                           "unit": "TMAD32/s (v_mad_u64_u32, algorithmic)",
+                           "frac": work / (ms * 1e-3) / PEAK_MAD32_PER_S, "traffic": None,
+                           "kernel": "k_g2_mul_split", "per_launch_ms": ms,
+                           "basis": "SURVEY.md 8(f1): ~9,165 Fq-mul per G2*Fr (253 doublings + ~127 additions of the "
+                                    "reference chain, Fq2 products counted as 3 Fq-mul), x128 MAD32"}
+        m = min(args.cpu_sample or 512, n)
+        threads = host_cpus()["usable"]
+        ph, kh, oh = (t[:m].cpu().numpy().view(np.uint64) for t in (P, k2, out))
+        t0 = time.perf_counter()
+        ref = O.g2_mul(ph, kh, threads)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": m / dt, "unit": unit, "cores": threads, "kind": "port",
+                               "sample": "%d G2*Fr of the bench inputs, oracle, %d threads" % (m, threads),
+                               "parity_sample_bit_exact": bool(np.array_equal(ref, oh))}
     elif args.workload == "g1mul":
         # ~3,800 Fq-mul per random 254-bit scalar (253 doublings x 7 + ~127 additions
         # x 16), x128 MAD32; the kernel is the only launch of the step (HIP events on its stream)
@@ -860,10 +889,10 @@ def main():
     ap.add_argument("--dry-run-cpu", action="store_true",
                     help="control-flow check on CPU: gloo + a stub engine (no pairing is computed)")
     ap.add_argument("--workload", default="pairing",
-                    choices=["pairing", "g1mul", "product", "g2validate", "g2decompress", "gtpow"],
+                    choices=["pairing", "g1mul", "g2mul", "product", "g2validate", "g2decompress", "gtpow"],
                     help="pairing: configs 2/4 (default); g1mul: config 3 (2^18 G1*Fr); product: config 5 "
-                         "(2^14-term pairing_batch); SURVEY 8(f): g2validate (AffineG2::new incl. the order "
-                         "check), g2decompress (G2::from_compressed), gtpow (Gt::pow(Fr)), 2^16 each")
+                         "(2^14-term pairing_batch); SURVEY 8(f): g2mul (G2*Fr), g2validate (AffineG2::new incl. "
+                         "the order check), g2decompress (G2::from_compressed), gtpow (Gt::pow(Fr)), 2^16 each")
     args = ap.parse_args()
     if args.config is None:
         args.config = 2 if args.gpus == 1 else 4

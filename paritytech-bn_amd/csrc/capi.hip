@@ -563,7 +563,14 @@ static void g1_mul_launch(const bn_g1* d_p, const bn_fr* d_k, size_t n, bn_g1* d
         k_g1_mul<<<grid_for(n), kBlock, 0, s>>>(d_p, d_k, n, d_out);
 }
 static void g2_mul_launch(const bn_g2* d_p, const bn_fr* d_k, size_t n, bn_g2* d_out, hipStream_t s) {
-    k_g2_mul<<<grid_for(n), kBlock, 0, s>>>(d_p, d_k, n, d_out);
+    static const bool split = [] {  // A/B (temporary): off until measured on the GPU
+        const char* e = getenv("BN254MI_G2_SPLIT");
+        return e && atoi(e) != 0;
+    }();
+    if (split)
+        k_g2_mul_split<<<grid_pair(kPathLanes * n), kPairBlock, 0, s>>>(d_p, d_k, n, d_out);
+    else
+        k_g2_mul<<<grid_for(n), kBlock, 0, s>>>(d_p, d_k, n, d_out);
 }
 
 template <typename P, typename K>
@@ -1213,7 +1220,7 @@ int bn_g2_mul_many_dev(bn_ctx* c, const bn_g2* d_p, const bn_fr* d_k, size_t n, 
     CTX_GUARD(c);
     if (n == 0) return BN_OK;
     if (!d_p || !d_k || !d_out) return fail(c, BN_ERR_INVALID_ARGUMENT, "null buffer");
-    k_g2_mul<<<grid_for(n), kBlock, 0, pick(c, stream)>>>(d_p, d_k, n, d_out);
+    g2_mul_launch(d_p, d_k, n, d_out, pick(c, stream));
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }

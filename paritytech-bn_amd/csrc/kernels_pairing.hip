@@ -243,6 +243,28 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
     st_fq12(out, kL * plan.S * G, l, f);
 }
 
+// G2 * Fr (mod.rs:272-292) on the pairing path's two-lane layout: the chain of
+// curve.h jac_mul with lane 2i + c holding coordinate c of element i, so a batch
+// is twice the waves of the one-lane k_g2_mul and each lane holds half the state.
+// Both lanes of an element follow the same scalar, so the ballot schedule's
+// decisions are the one-lane kernel's.  Launched with kPairBlock threads per
+// block (kernels.h: issue balance).
+__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_g2_mul_split(const bn_g2* __restrict__ p,
+                                                                         const bn_fr* __restrict__ k, size_t n,
+                                                                         bn_g2* __restrict__ out) {
+    fold_table_init();
+    const Balance bal = balance_init();
+    const size_t l = lane_id(), i = l / kL;
+    if (i >= n) return;
+    uint32_t s[8];
+    fr_to_canonical(k[i], s);
+    const G2J a = {widen<kPt>(ld_ref2(p[i].x)), widen<kPt>(ld_ref2(p[i].y)), widen<kPt>(ld_ref2(p[i].z))};
+    const G2J r = jac_mul(a, s, [&](int t) { balance_step(bal, (uint32_t)t); });
+    st_ref2(out[i].x, r.x);
+    st_ref2(out[i].y, r.y);
+    st_ref2(out[i].z, r.z);
+}
+
 }  // namespace bn
 
 BN_EXPORT_FOLD_CHECK(pairing)

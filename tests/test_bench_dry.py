@@ -85,3 +85,6 @@ def test_bench_capi_form_rejects_launcher_and_workloads():
     assert r.returncode == 2 and "--form capi" in r.stderr
     r = run(["--form", "capi", "--workload", "g1mul", "--dry-run-cpu"])
     assert r.returncode == 2
+    r = run(["--workload", "g2mul", "--gpus", "2", "--dry-run-cpu"], env={"WORLD_SIZE": "2", "RANK": "0",
+                                                                      "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "runs on one GPU" in r.stderr
