@@ -1,5 +1,6 @@
-// kernels_group.hip -- batched G1/G2 scalar multiplication (mod.rs:272-292) and
-// the group law (mod.rs:169-216, 294-358), one lane per element.
+// kernels_group.hip -- batched G1 scalar multiplication (mod.rs:272-292) and the
+// G1/G2 group law (mod.rs:169-216, 294-358), one lane per element (G2 * Fr runs
+// on the two-lane layout: kernels_pairing.hip k_g2_mul_split).
 // fq_fold reads -q*p from an LDS table (fq.h; every kernel here calls
 // fold_table_init first)
 #ifndef BN_FOLD_LDS
@@ -100,20 +101,6 @@ __global__ void __launch_bounds__(kPairBlock) k_g1_mul2(const bn_g1* __restrict_
         st_ref(out[j].z, r1.z);
     }
 }
-__global__ void __launch_bounds__(kBlock) k_g2_mul(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n,
-                                                   bn_g2* __restrict__ out) {
-    fold_table_init();
-    const size_t i = lane_id();
-    if (i >= n) return;
-    uint32_t s[8];
-    fr_to_canonical(k[i], s);
-    G2J a = {widen<kPt>(ld_ref2(p[i].x)), widen<kPt>(ld_ref2(p[i].y)), widen<kPt>(ld_ref2(p[i].z))};
-    G2J r = jac_mul(a, s);
-    st_ref2(out[i].x, r.x);
-    st_ref2(out[i].y, r.y);
-    st_ref2(out[i].z, r.z);
-}
-
 // ---------------------------------------------------------------- group law
 // Group::normalize (lib.rs:391-398, 542-549): to_affine (mod.rs:199-216), then
 // to_jacobian (mod.rs:220-226: z = one); a zero point stays as it is.  The

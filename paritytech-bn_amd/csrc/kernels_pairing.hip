@@ -245,7 +245,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
 
 // G2 * Fr (mod.rs:272-292) on the pairing path's two-lane layout: the chain of
 // curve.h jac_mul with lane 2i + c holding coordinate c of element i, so a batch
-// is twice the waves of the one-lane k_g2_mul and each lane holds half the state.
+// is twice the waves of a one-lane kernel (rounds 1-3) and each lane holds half the state.
 // Both lanes of an element follow the same scalar, so the ballot schedule's
 // decisions are the one-lane kernel's.  Launched with kPairBlock threads per
 // block (kernels.h: issue balance).
