@@ -31,7 +31,7 @@ timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_g1_fetch -o p -- pyth
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_g1_write -o p -- python3 bench.py --workload g1mul --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_g1_write.err
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_g1_sq -o p -- python3 bench.py --workload g1mul --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_g1_sq.err
 echo "== workloads"
-for w in g1mul product gtpow g2validate g2decompress; do
+for w in g1mul g2mul product gtpow g2validate g2decompress; do
   timeout -k 10 300 python -u bench.py --workload $w --steps 10 --warmup 2 > $OUT/bench_$w.json 2> $OUT/bench_$w.err
   head -c 300 $OUT/bench_$w.json; echo
 done
