@@ -98,9 +98,9 @@ summary = {}
 # SURVEY.md 8(d) generic Fq-mul counts per element of the bench's kernels, and how many
 # elements one wave carries (the pairing path runs two lanes per pairing)
 ALG_FQMUL = {"k_pairing_full": 19 + 2655 + 6045 + 8767, "k_pairing_fused": 19 + 2655 + 6045, "k_prepare": 19 + 2655, "k_miller": 6045, "k_fq12_vm": 8767,
-             "k_g1_mul": 3800, "k_g1_mul2": 3800, "k_g2_mul": 9165}
+             "k_g1_mul": 3800, "k_g1_mul2": 3800, "k_g2_mul": 9165, "k_g2_mul_split": 9165}
 ELEMS_PER_WAVE = {"k_pairing_full": 32, "k_pairing_fused": 32, "k_prepare": 32, "k_miller": 32, "k_fq12_vm": 32, "k_fe_out": 32,
-                  "k_g1_mul2": 128}
+                  "k_g1_mul2": 128, "k_g2_mul_split": 32}
 lines = ["%-16s %14s %14s %14s %12s %10s" % ("kernel", "FETCH_bytes", "WRITE_bytes", "VALU/wave", "WAVE_CYC/w",
                                                  "VALU/cyc")]
 for k, v in sorted(agg.items()):
