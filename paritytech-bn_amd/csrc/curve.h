@@ -313,9 +313,10 @@ BN_INLINE Jac<F> jac_mul(const Jac<F>& p, const uint32_t k[8], Step&& step = Ste
 // Two chains per lane (p0*k0 and p1*k1): each iteration still runs ONE kind of step
 // for the wave, but a lane serves it from whichever of its chains is ready for it
 // (the one with more bits left when both are) -- the ballot sees twice the
-// candidates, so fewer lanes idle in each step (a simulation of 64 lanes of random
-// scalars: 1.41x the chains' own Fq-mul weight for one chain per lane, 1.21x for
-// two).  Each chain's own steps keep their order: both outputs stay bit-exact.
+// candidates, so fewer lanes idle in each step (measured on config 3's launch with
+// the counter build: 1.289x the chains' own Fq-mul weight, against 1.407x for one
+// chain per lane; the addition here weighs 16, its base's z^2, z^3 recomputed).
+// Each chain's own steps keep their order: both outputs stay bit-exact.
 // `base(c)` returns the base of chain c (0/1); the kernel keeps the two bases in
 // LDS, so the loop holds two accumulators in registers, not four points.
 // `bit(c, i)` returns bit i of chain c's canonical scalar and `top0`/`top1` are the
