@@ -315,17 +315,18 @@ constexpr int kRegionA = 1, kRegionB = 2;  // ping-pong regions of the product r
 constexpr int kRegionParts = 3;            // per-chunk partial products
 constexpr int kRegionResult = 4;           // the final product (element 0, stride 1)
 constexpr size_t kWideGroups = kBlock / 16;  // k_fq12_reduce_wide: 16-lane groups per block
-constexpr size_t kReduceBlocksMax = 512;      // two rounds of 256-thread blocks (one per CU: 248 + 32 registers)
+constexpr size_t kReduceBlocksMax = 512;      // one round of 256-thread blocks, two per CU (kernels_reduce.hip)
 
 // Multiply each of `sets` sets of n split-layout values together on the wide
 // layout (k_fq12_reduce_wide, all sets in one launch per level): set y is
 // elements y * in_set + [0, n) of `in` (stride in_stride), its product goes to
 // element out_base + y * out_set of `out` (stride out_stride).  `in` must not
 // be a ping-pong region.  Each level's chain length per group G is the smallest
-// power of two >= 2 that needs at most two rounds of blocks on the CUs: config
-// 5's 16 x 4,096 segment values take two launches (G = 8, then 2) instead of
-// three of G = 2 -- 2.20 against 2.25-2.26 ms per product; one round (G = 16)
-// 2.21-2.27, G = 32 2.27-2.30 (profiles/r4e_ab_reduce.txt).
+// power of two >= 2 that needs at most 512 blocks: config 5's 16 x 4,096
+// segment values take two launches (G = 8, then 2) instead of three of G = 2 --
+// 2.20 against 2.25-2.26 ms per product; G = 16 2.21-2.27, G = 32 2.27-2.30
+// (profiles/r4e_ab_reduce.txt, one block per CU then); with two blocks per CU
+// (kernels_reduce.hip) G = 8 stays ahead of G = 4 (profiles/r4q_ab_reduce_lds.txt).
 int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, size_t n, size_t in_set, int sets, uint32_t* out,
                  size_t out_stride, size_t out_base, size_t out_set, hipStream_t s) {
     const uint32_t* src = in;

@@ -115,52 +115,8 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
     if (w.l < 12 && live) st_words(&out[e].c[w_gt_index(w)], words);
 }
 
-// Product reduction of several independent sets (blockIdx.y = set y, the
-// elements y * in_set + [0, n) of `in`, split layout, stride in_stride): block
-// (b, y) multiplies the set's elements [16Gb, 16Gb + 16G) (G = per_group) -- a
-// chain of G factors per group (elements g, g + 16, ...), then a tree over the 16
-// groups through LDS --
-// and writes the block's product as element out_base + y * out_set + b of `out`
-// (stride out_stride).  Elements past n count as one.  The order of the factors
-// differs from the reference's left-to-right accumulation; Fq12 multiplication
-// is commutative and associative, so the value is the same.
-__shared__ uint32_t g_wval[kWGroups * kWLanes * kWSlot];  // 12 KB: one value per group
-
-__global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
-                                                             size_t n, size_t in_set, uint32_t* __restrict__ out,
-                                                             size_t out_stride, size_t out_base, size_t out_set,
-                                                             int per_group) {
-    fold_table_init();
-    const WL w = wl();
-    const int g = (int)threadIdx.x / kWLanes;
-    // group g multiplies elements e0 + 16t (t < per_group) of its block's range in
-    // a chain -- at each step the block's 16 groups read 16 consecutive elements --
-    // with the next factor's load issued before the product that precedes it
-    // (factors past n are skipped), then the groups' values meet in the tree below
-    const size_t e0 = (size_t)blockIdx.x * kWGroups * (size_t)per_group + g, sb = (size_t)blockIdx.y * in_set;
-    const Fq<2> one = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
-    Fq<2> x = e0 < n ? w_ld_split(in, in_stride, sb + e0, w) : one;
-    Fq<2> y = e0 + kWGroups < n ? w_ld_split(in, in_stride, sb + e0 + kWGroups, w) : one;
-#pragma unroll 1
-    for (int t = 1; t < per_group; ++t) {
-        const size_t e = e0 + (size_t)(t + 1) * kWGroups;
-        const Fq<2> y_next = (t + 1 < per_group && e < n) ? w_ld_split(in, in_stride, sb + e, w) : one;
-        if (e0 + (size_t)t * kWGroups < n) x = w12_mul(x, y);  // uniform per group
-        y = y_next;
-    }
-    uint32_t* mine = g_wval + (g * kWLanes) * kWSlot;
-#pragma unroll 1
-    for (int s = kWGroups / 2; s >= 1; s /= 2) {
-        w_put(mine, w.l, x);
-        __syncthreads();
-        if (g < s) {
-            const Fq<2> y2 = w_get<2>(g_wval + ((g + s) * kWLanes) * kWSlot, w.l);
-            x = w12_mul(x, y2);
-        }
-        __syncthreads();
-    }
-    if (g == 0) w_st_split(out, out_stride, out_base + blockIdx.y * out_set + blockIdx.x, w, x);
-}
+// one value per group for k_horner_tree's product tree
+__shared__ uint32_t g_wval[kWGroups * kWLanes * kWSlot];  // 12 KB
 
 // Recombination of segmented Miller loops (pairing.h miller_segment), one
 // 16-lane group per element e < n: segment s of element e is element s * n + e
