@@ -23,7 +23,7 @@ os.environ.setdefault("BN254MI_LIB", os.path.join(ROOT, "paritytech-bn_amd", "li
 
 from substrate_bn import _native, synth  # noqa: E402
 
-TUS = ["pairing", "fe", "group", "gtpow", "codec", "util"]
+TUS = ["pairing", "fe", "group", "gtpow", "codec", "util", "reduce"]
 
 
 def counters(L):
