@@ -23,7 +23,7 @@ os.environ.setdefault("BN254MI_LIB", os.path.join(ROOT, "paritytech-bn_amd", "li
 
 from substrate_bn import _native, synth  # noqa: E402
 
-TUS = ["pairing", "fe", "group", "gtpow", "codec", "util", "reduce"]
+TUS = ["fe", "group", "gtpow", "codec", "util", "reduce"]  # kernels_pairing: product build (Makefile dbg)
 
 
 def counters(L):
@@ -46,6 +46,7 @@ def main():
     q = ctx.g2_mul_many(g2, synth.fr_images(n, 2))
     gt = ctx.pairing_many(p, q)
     ctx.pairing_batch(p[:1024], q[:1024])
+    ctx.pairing_batch(np.tile(p, (4, 1)), np.tile(q, (4, 1)))  # segmented product: reduction chains of 8
     ctx.miller_loop_many(p[:256], q[:256])
     ctx.gt_pow_many(gt, synth.fr_images(n, 3, lo=0))
     for op in ("mul", "sqr", "inv", "cyc_sqr", "exp_by_neg_z", "frob1", "frob2", "frob3"):
