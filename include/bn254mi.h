@@ -64,7 +64,8 @@ void* bn_ctx_stream(bn_ctx* ctx);
  * bn_pairing_many_allgather_dev): synchronizes `stream` (NULL: the context's stream), returns
  * BN_ERR_INTERNAL or BN_ERR_FE_ZERO (a Miller value was zero: the reference panics, mod.rs:900)
  * if any such call since the last bn_dev_status (or host-buffer call, which starts from a clear
- * word) set it, else BN_OK, and clears it.  On a multi-device context it checks every device. */
+ * word) set it, else BN_OK, and clears it.  On a multi-device context it checks every device,
+ * each on its own context stream, and `stream` must be NULL (else BN_ERR_INVALID_ARGUMENT). */
 int bn_dev_status(bn_ctx* ctx, void* stream);
 
 /* ---- several devices of the node in one process ----

@@ -420,10 +420,6 @@ SegPlan seg_plan(size_t n) {
 SegPlan batch_plan(size_t n) {
     int K = 1;
     while (K < 16 && (size_t)kMaxSeg * ((n + 2 * K - 1) / (2 * K)) >= ((size_t)1 << 16)) K *= 2;
-    if (const char* e = getenv("BN254MI_BATCH_K")) {  // A/B: pairs per lane pair (1, 2, 4, 8, 16)
-        const int v = atoi(e);
-        if (v >= 1 && v <= 16) K = v;
-    }
     return cut_plan(kMaxSeg, K);
 }
 
@@ -479,11 +475,12 @@ int finish_product(bn_ctx* c, const SegPlan& plan, size_t nchunks, int do_fe, bn
 // values): the one-wave build while its blocks (8 pairs each, one per CU) fit one
 // round, above that the two-wave build (kernels_latency_w2.hip: two blocks per CU),
 // unless $BN254MI_LATENCY_W2=0 (A/B)
-constexpr size_t kLatW1Max = 2048;
+// (lat_w1_max = the device's CU count x kLatPairs, set at context creation: 2,048
+// on MI355X's 256 CUs)
 static void launch_latency(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, bn_gt* out, uint32_t* f_out,
                            int mode, hipStream_t s) {
     const unsigned blocks = (unsigned)((m + kLatPairs - 1) / kLatPairs);
-    if (m <= kLatW1Max || !c->latency_w2)
+    if (m <= c->lat_w1_max || !c->latency_w2)
         k_pairing_latency<<<blocks, kLatThreads, 0, s>>>(d_p, d_q, m, out, f_out, mode, c->d_err);
     else
         k_pairing_latency_w2<<<blocks, kLatThreads, 0, s>>>(d_p, d_q, m, out, f_out, mode, c->d_err);
@@ -654,6 +651,11 @@ int bn_ctx_create(int device, bn_ctx** out) {
     c->latency_max = kLatencyMaxDefault;
     if (const char* e = getenv("BN254MI_LATENCY_MAX")) c->latency_max = (size_t)strtoull(e, nullptr, 10);
     if (const char* e = getenv("BN254MI_LATENCY_W2")) c->latency_w2 = atoi(e) != 0;
+    {  // one block of kLatPairs pairs per CU: the one-wave latency build's single round
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->lat_w1_max = (size_t)cus * kLatPairs;
+    }
     c->prepare_wide_max = kPrepareWideMaxDefault;
     if (const char* e = getenv("BN254MI_PREPARE_WIDE_MAX")) c->prepare_wide_max = (size_t)strtoull(e, nullptr, 10);
     Prog P;
@@ -838,6 +840,12 @@ int bn_pairing_many_dev(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n,
 
 int bn_dev_status(bn_ctx* c, void* stream) {
     if (c && !c->subs.empty()) {
+        // one caller stream cannot order the work of several devices: each device is
+        // checked on its own context stream (ws_event orders it after every _dev call)
+        if (stream) {
+            std::lock_guard<std::mutex> g(c->err_mu);
+            return fail(c, BN_ERR_INVALID_ARGUMENT, "bn_dev_status: stream must be NULL on a multi-device context");
+        }
         int rc = BN_OK;
         for (bn_ctx* d : c->subs) {
             const int r = bn_dev_status(d, nullptr);
@@ -1377,9 +1385,12 @@ int bn_g2_from_compressed_many_dev(bn_ctx* c, const uint8_t* d_b, size_t n, bn_g
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
-// Gt::pow: the per-lane window table lives in the context's Fq12 slots (16 of kFeSlots);
-// k_gt_pow addresses a lane's entry by a 32-bit buffer offset (ld_fq12_buf_sel)
-static_assert(16ull * kSlotWords * kChunk * 4 + (size_t)kSlotWords * kChunk * 4 < (1ull << 31),
+// Gt::pow: the per-lane window table lives in the context's Fq12 slots (kGtPowEntries
+// of kFeSlots); k_gt_pow addresses a lane's entry by a 32-bit buffer offset
+// (ld_fq12_buf_sel): entry t < kGtPowEntries starts at t * kSlotWords * kChunk * 4
+// bytes and its lane copies lie below (t + 1) * kSlotWords * kChunk * 4
+static_assert(kGtPowEntries <= kFeSlots, "k_gt_pow's window table must fit the context's Fq12 slots");
+static_assert((unsigned long long)kGtPowEntries * kSlotWords * kChunk * 4 < (1ull << 31),
               "k_gt_pow window-table offsets must fit the buffer descriptor's 31-bit range");
 int bn_gt_pow_many_dev(bn_ctx* c, const bn_gt* d_a, const bn_fr* d_k, size_t n, bn_gt* d_out, void* stream) {
     CTX_GUARD(c);

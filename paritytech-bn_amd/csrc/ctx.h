@@ -43,7 +43,8 @@ struct bn_ctx {
     int miller_form = 3;  // 3: k_pairing_full; 1: k_pairing_fused + k_fq12_vm + k_fe_out; 0/2: k_prepare + k_miller(_seg) + ...
     // bn_pairing_many_dev batches of at most this many pairs run k_pairing_latency
     size_t latency_max = 0;
-    bool latency_w2 = true;  // above 2,048 pairs the one-launch path runs the two-wave build
+    bool latency_w2 = true;  // above lat_w1_max pairs the one-launch path runs the two-wave build
+    size_t lat_w1_max = 2048;  // CU count x kLatPairs (bn_ctx_create): one round of one-wave blocks
     // batches of at most this many pairs take k_prepare_wide (8 lanes per pair)
     size_t prepare_wide_max = 0;
     int* d_err = nullptr;

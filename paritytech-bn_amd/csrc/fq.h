@@ -206,6 +206,26 @@ BN_INLINE Fq<kv(K)> fq_neg(const Fq<K>& a_in) {
     return fq_norm(Fq<kenc(B, 2)>{{r.v[0], r.v[1], r.v[2], r.v[3], r.v[4], r.v[5], r.v[6], r.v[7], r.v[8]}});
 }
 
+// ---------------------------------------------------------------- single-chain column sums
+// BN_DOT2_ASM (device code): fq_mul, fq_sqr and fq2_split.h fq_dot2 run the
+// hand-scheduled product scan of dot2_asm.inc (tools/gen_dot2_asm.py): one
+// v_mad_u64_u32 chain per product, each column started from the previous
+// column's carry, so no carry-merge instruction per column.  The same column
+// sums in another association order: identical digits.
+#ifndef BN_DOT2_ASM
+#define BN_DOT2_ASM 0
+#endif
+#if BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
+#include "dot2_asm.inc"
+#define BN_ASM_OUT9(a) "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(a[4]), "=&v"(a[5]), \
+                       "=&v"(a[6]), "=&v"(a[7]), "=&v"(a[8])
+#define BN_ASM_IN9(a) "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "v"(a[8])
+#define BN_ASM_P                                                                                              \
+    "s"(kP29.v[0]), "s"(kP29.v[1]), "s"(kP29.v[2]), "s"(kP29.v[3]), "s"(kP29.v[4]), "s"(kP29.v[5]),        \
+        "s"(kP29.v[6]), "s"(kP29.v[7]), "s"(kP29.v[8]), "s"((uint32_t)BN_PINV29)
+#define BN_ASM_CLOBBER "vcc", "v2", "v3"
+#endif
+
 // ---------------------------------------------------------------- column accumulator
 // The digit products of several Fq products summed by columns in 17 64-bit
 // accumulators and reduced once (fq12_wide.h's twelve-product sums).  Measured
@@ -274,8 +294,12 @@ BN_INLINE auto fq_mul(const Fq<A>& a_in, const Fq<B>& b_in) {
     static_assert((long long)kv(A) * kv(B) <= 160 * 160, "product bound");
     const Fq<A>& a = a_in;
     const Fq<B>& b = b_in;
-    uint32_t m[9];
     Fq<mul_bound(kv(A), kv(B))> r;
+#if BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
+    asm(BN_ASM_MUL : BN_ASM_OUT9(r.v) : BN_ASM_IN9(a.v), BN_ASM_IN9(b.v), BN_ASM_P : BN_ASM_CLOBBER);
+    return r;
+#endif
+    uint32_t m[9];
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 17; ++k) {
@@ -313,8 +337,12 @@ BN_INLINE auto fq_sqr(const Fq<B>& a_in) {
     uint32_t d[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
-    uint32_t m[9];
     Fq<mul_bound(kv(B), kv(B))> r;
+#if BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
+    asm(BN_ASM_SQR : BN_ASM_OUT9(r.v) : BN_ASM_IN9(a.v), BN_ASM_IN9(d), BN_ASM_P : BN_ASM_CLOBBER);
+    return r;
+#endif
+    uint32_t m[9];
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 17; ++k) {
@@ -416,9 +444,17 @@ BN_INLINE auto fq_half(const Fq<K>& a_in) {
 #endif
 #if BN_DEVICE_CHECKS && defined(__HIPCC__)
 static __device__ unsigned g_fold_bad;
-#define BN_FOLD_CHECK(q, B)                                                          \
-    do {                                                                             \
-        if ((q) > (uint32_t)kv(B)) atomicAdd(&g_fold_bad, 1u);                       \
+// The counter is bumped in a function of its own: with the atomic inlined into
+// every fold, the backend emitted an illegal VOPC for kernels_pairing.hip
+// ("Operand has incorrect register class", V_CMP_NE_U32_e32 0, src_shared_base),
+// which kept that unit out of the checked build in rounds 3-4.
+static __device__ __noinline__ void fold_bad_hit() {
+    __hip_atomic_fetch_add((__attribute__((address_space(1))) unsigned*)&g_fold_bad, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+#define BN_FOLD_CHECK(q, B)                                \
+    do {                                                   \
+        if ((q) > (uint32_t)kv(B)) fold_bad_hit();         \
     } while (0)
 #else
 #define BN_FOLD_CHECK(q, B) ((void)0)

@@ -478,15 +478,31 @@ static_assert(kZNaf.top == 62 && kZNaf.n == 24, "NAF of u");
 #endif
 constexpr int kDuoRing = BN_DUO_RING;             // S -> M items in flight
 constexpr int kDuoWords = (kDuoRing + 2) * kWArr;  // channel words per element
-constexpr uint32_t kDuoSpinCap = 1u << 26;        // ~4 s of s_sleep 1: never reached while both run
+// The cap of every capped LDS hand-off wait (here and latency_kernel.h): ~4 s of
+// s_sleep 1, never reached while both sides run.  A build parameter so that the
+// failure-path library (`make -C paritytech-bn_amd cap0`, BN_SPIN_CAP=0) trips
+// the waits deterministically and tests/test_gpu_failure.py can check that the
+// call then fails with BN_ERR_INTERNAL instead of returning a value.
+#ifndef BN_SPIN_CAP
+#define BN_SPIN_CAP (1u << 26)
+#endif
+constexpr uint32_t kSpinCap = BN_SPIN_CAP;
+constexpr uint32_t kDuoSpinCap = kSpinCap;
 
 // A wait that runs out of its cap would go on to read a slot that was never
 // published: it sets the BN_ERR_INTERNAL bit of *err, so the call fails
-// (check_err, bn_dev_status) instead of returning a wrong Gt.
-__device__ __forceinline__ void duo_wait(const volatile uint32_t* c, uint32_t v, int* err) {
+// (check_err, bn_dev_status) instead of returning a wrong Gt.  The outcome is
+// decided on the counter itself (a counter that arrived during the last sleep
+// is a success), and `dead` makes it sticky for the wave: after one wait has run
+// out, the later ones do not spin again (the call has failed already).
+__device__ __forceinline__ void duo_wait(const volatile uint32_t* c, uint32_t v, int* err, bool& dead) {
     uint32_t spins = 0;
-    for (; *c < v && spins < kDuoSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
-    if (spins == kDuoSpinCap && err) atomicOr(err, 1 << BN_ERR_INTERNAL);
+    if (!dead)
+        for (; *c < v && spins < kDuoSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
+    if (*c < v) {
+        dead = true;
+        if (err) atomicOr(err, 1 << BN_ERR_INTERNAL);
+    }
     asm volatile("" ::: "memory");
 }
 __device__ __forceinline__ void duo_signal(volatile uint32_t* c, uint32_t v) {
@@ -498,13 +514,14 @@ struct WDuo {
     volatile uint32_t* cnt;  // three counters, zero at the start
     uint32_t items, results;
     int* err;  // device error word: BN_ERR_INTERNAL when a wait runs out of its cap
+    bool dead = false;  // a wait of this wave has run out of its cap (duo_wait)
     __device__ void put(const Fq<2>& x) {  // S
-        if (items >= (uint32_t)kDuoRing) duo_wait(cnt + 1, items + 1 - kDuoRing, err);
+        if (items >= (uint32_t)kDuoRing) duo_wait(cnt + 1, items + 1 - kDuoRing, err, dead);
         w_put(ch + (items % kDuoRing) * kWArr, (int)(threadIdx.x & (kWLanes - 1)), x);
         duo_signal(cnt, ++items);
     }
     __device__ Fq<2> take() {  // M
-        duo_wait(cnt, items + 1, err);
+        duo_wait(cnt, items + 1, err, dead);
         const Fq<2> x = w_get<2>(ch + (items % kDuoRing) * kWArr, (int)(threadIdx.x & (kWLanes - 1)));
         duo_signal(cnt + 1, ++items);
         return x;
@@ -514,7 +531,7 @@ struct WDuo {
         duo_signal(cnt + 2, ++results);
     }
     __device__ Fq<2> get_result() {  // S
-        duo_wait(cnt + 2, results + 1, err);
+        duo_wait(cnt + 2, results + 1, err, dead);
         const Fq<2> x = w_get<2>(ch + (kDuoRing + results % 2) * kWArr, (int)(threadIdx.x & (kWLanes - 1)));
         ++results;
         return x;

@@ -171,8 +171,13 @@ template <int X, int Y, int Z, int W>
 BN_INLINE auto fq_dot2(const Fq<X>& x, const Fq<Y>& y, const Fq<Z>& z, const Fq<W>& w) {
     static_assert(kl(X) * kl(Y) + kl(Z) * kl(W) <= 6, "fq_dot2: column sum could overflow 64 bits");
     constexpr int BO = 1 + (int)(((long long)kv(X) * kv(Y) + (long long)kv(Z) * kv(W)) * 5908 / 1000000 + 1);
-    uint32_t m[9];
     Fq<BO> r;
+#if BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
+    asm(BN_ASM_DOT2 : BN_ASM_OUT9(r.v) : BN_ASM_IN9(x.v), BN_ASM_IN9(y.v), BN_ASM_IN9(z.v), BN_ASM_IN9(w.v), BN_ASM_P
+        : BN_ASM_CLOBBER);
+    return r;
+#endif
+    uint32_t m[9];
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 17; ++k) {

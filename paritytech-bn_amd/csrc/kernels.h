@@ -29,6 +29,10 @@ constexpr int kSlotLaneWords = BN_SPLIT ? 54 : 108;
 constexpr int kCoeffFq = BN_NUM_COEFFS * 6;  // Fq elements of line coefficients per pairing
 constexpr size_t kChunk = size_t(1) << 18;   // pairings per launch set (~5 GB workspace)
 constexpr int kSlotWords = 108;              // one Fq12: 12 Fq x 9 digits
+// Gt::pow's window table (kernels_gtpow.hip): x^0..x^16 for the signed 5-bit
+// windows of cyclotomic-subgroup waves (x^0..x^15 otherwise), in the context's
+// Fq12 slots
+constexpr int kGtPowEntries = 17;
 
 // ---------------------------------------------------------------- lane-strided storage
 template <int B>

@@ -12,8 +12,9 @@
 //  - A wave of cyclotomic-subgroup members (see below): signed 5-bit windows
 //    (Booth recoding, digits -16..16 read straight off six scalar bits; a
 //    negative digit multiplies by the conjugate, which is the inverse there):
-//    table x^0..x^16, 250 cyclotomic squarings and 50 products -- 64 products in
-//    all against the unsigned 4-bit chain's 77.
+//    table x^0..x^16 (kGtPowEntries, 15 products to build), 250 cyclotomic
+//    squarings and 50 window products -- 65 products in all against the
+//    unsigned 4-bit chain's 14 + 63 = 77.
 //  - Otherwise: unsigned 4-bit windows, table x^0..x^15, 252 generic squarings
 //    and 63 products.
 //
@@ -77,7 +78,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_gt_pow(const bn_gt*
         st_fq12_buf(slot(1, nn), nn, l, x);
     }
     Fq12<kF> t = x;
-    const uint32_t entries = cyc ? 17u : 16u;
+    const uint32_t entries = cyc ? (uint32_t)kGtPowEntries : 16u;
 #pragma unroll 1
     for (uint32_t j = 2; j < entries; ++j) {
         balance_step(bal, j);

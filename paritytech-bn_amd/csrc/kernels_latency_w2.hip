@@ -18,3 +18,5 @@
 #include "fq12_wide.h"
 #include "lines_wide.h"
 #include "latency_kernel.h"
+
+BN_EXPORT_FOLD_CHECK(latency_w2)

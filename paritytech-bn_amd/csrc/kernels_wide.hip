@@ -291,3 +291,5 @@ extern "C" int bn_dbg_hor_stamps(uint64_t out[8]) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(bn::g_hor_stamps), 8 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
 }
 #endif
+
+BN_EXPORT_FOLD_CHECK(wide)

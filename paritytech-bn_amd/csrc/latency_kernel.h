@@ -46,7 +46,7 @@ namespace bn {
 __shared__ uint32_t g_lat_prod[kLatPairs], g_lat_cons[kLatPairs], g_lat_skip[kLatPairs];
 __shared__ uint32_t g_lat_duo[kLatPairs * 4];  // BN_FE_DUO: the counters of each pair's channel
 static_assert(kDuoWords <= kLatRing * kLatLineWords, "the FE channel reuses the pair's line ring");
-constexpr uint32_t kLatSpinCap = 1u << 26;  // ~4 s of s_sleep 1: never reached while both sides run
+constexpr uint32_t kLatSpinCap = kSpinCap;  // fq12_wide.h: ~4 s of s_sleep 1, never reached while both sides run
 
 // Diagnostic build (-DBN_LAT_STAMPS=1, tools/lat_stamps.py): block 0 records
 // s_memrealtime (100 MHz) at the phase boundaries of its first pair into a
@@ -107,6 +107,7 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
         const PairAffine a = pair_to_affine(p, q, pi, pi * kL + c, nullptr, err, valid ? mode : 0);
         LAT_STAMP(threadIdx.x == 0, 1);  // producer: to_affine done
         if (st && c == 0) g_lat_skip[j] = a.skip ? 1u : 0u;
+        bool dead = false;  // a wait of this wave ran out of its cap
         auto emit = [&](int line, const Ell& e) {
             // slots 0, 2 scale ell_vw by Py, slots 1, 3 ell_vv by Px (one product
             // per lane instead of two); slot 0 takes x2 from slot 1
@@ -115,9 +116,13 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
             const auto x4 = y;
             const auto x2 = pw_from(y, 1);
             uint32_t spins = 0;
-            for (; BN_ANY(valid && line - (int)cons[j] >= kLatRing) && spins < kLatSpinCap; ++spins)
-                __builtin_amdgcn_s_sleep(1);
-            if (spins == kLatSpinCap && L == 0 && err) atomicOr(err, 1 << BN_ERR_INTERNAL);  // ring overrun: fail the call
+            if (!dead)
+                for (; BN_ANY(valid && line - (int)cons[j] >= kLatRing) && spins < kLatSpinCap; ++spins)
+                    __builtin_amdgcn_s_sleep(1);
+            if (BN_ANY(valid && line - (int)cons[j] >= kLatRing)) {  // ring overrun: fail the call
+                dead = true;  // sticky for the wave: no later wait spins again
+                if (L == 0 && err) atomicOr(err, 1 << BN_ERR_INTERNAL);
+            }
             asm volatile("" ::: "memory");
             if (st) {  // the operand forms c0, c1, -c1 of each coefficient (fq12_wide.h w12_mul_line)
                 uint32_t* ln = g_lat_ring + (j * kLatRing + line % kLatRing) * kLatLineWords;
@@ -171,10 +176,15 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
     const size_t pi = live ? base + j : n - 1;
     const WL w = wl();
     auto ln = [&](int line) { return (uint32_t)((j * kLatRing + line % kLatRing) * kLatLineWords); };
+    bool dead = false;  // a wait of this group ran out of its cap
     auto wait_line = [&](int line) {
         uint32_t spins = 0;
-        for (; prod[j] <= (uint32_t)line && spins < kLatSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
-        if (spins == kLatSpinCap && w.l == 0 && err) atomicOr(err, 1 << BN_ERR_INTERNAL);  // line never published
+        if (!dead)
+            for (; prod[j] <= (uint32_t)line && spins < kLatSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
+        if (prod[j] <= (uint32_t)line) {  // line never published: fail the call
+            dead = true;
+            if (w.l == 0 && err) atomicOr(err, 1 << BN_ERR_INTERNAL);
+        }
         asm volatile("" ::: "memory");
     };
     auto took = [&](int line) {  // the line's words have been read (the product has returned)

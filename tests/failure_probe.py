@@ -1,0 +1,74 @@
+"""Child process of tests/test_gpu_failure.py (not collected by pytest).
+
+Runs with BN254MI_LIB = paritytech-bn_amd/libbn254mi_cap0.so: the product library
+with the capped LDS hand-off waits of the latency kernels and the two-group
+final exponentiation built at spin cap 0 (fq12_wide.h BN_SPIN_CAP), so that the
+first wait of each runs out.  Prints one JSON line with what every entry point
+returned; the test asserts on it.  The oracle is the checker only.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "paritytech-bn_amd"))
+
+from oracle import oracle as O  # noqa: E402
+from substrate_bn import _native  # noqa: E402
+
+
+def code_of(fn):
+    """BN_OK or the BnError code of fn(), plus its value when it returned."""
+    try:
+        return _native.BN_OK, fn()
+    except _native.BnError as e:
+        return e.code, None
+
+
+def main():
+    import torch
+    assert _native.LIB_PATH.endswith("libbn254mi_cap0.so"), _native.LIB_PATH
+    ctx = _native.Context(0)
+    n = 24
+    p, q, _, _ = O.random_pairs(n, seed=41, nthreads=8)
+    res = {}
+    # host-buffer forms: the latency kernel (n <= latency_max) -> BN_ERR_INTERNAL, no output
+    res["pairing_many"], v = code_of(lambda: ctx.pairing_many(p, q))
+    res["pairing_many_value_returned"] = v is not None
+    res["pairing_batch"], v = code_of(lambda: ctx.pairing_batch(p, q))
+    res["pairing_batch_value_returned"] = v is not None
+    res["miller_loop_batch"], _ = code_of(lambda: ctx.miller_loop_batch(q, p))
+    # the two-group final exponentiation of k_fe_wide (its S <-> M channel waits)
+    _, mv = O.miller_loop_batch(q[:1], p[:1])
+    f = np.tile(mv.reshape(1, 48), (4, 1))
+    res["final_exponentiation_many"], _ = code_of(lambda: ctx.final_exponentiation_many(f))
+    # device forms: the status-less bn_pairing_many_dev reports through bn_dev_status
+    dev = torch.device("cuda", 0)
+    P = torch.from_numpy(p.view(np.int64)).to(dev)
+    Q = torch.from_numpy(q.view(np.int64)).to(dev)
+    out = torch.zeros((n, 48), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    res["pairing_many_dev_call"], _ = code_of(lambda: ctx.pairing_many_dev(P.data_ptr(), Q.data_ptr(), n, out.data_ptr()))
+    res["dev_status_after"], _ = code_of(lambda: ctx.dev_status())
+    res["dev_status_cleared"], _ = code_of(lambda: ctx.dev_status())  # the sticky word was cleared
+    # bn_pairing_batch_dev with its device status word
+    st = torch.full((1,), -1, dtype=torch.int32, device=dev)
+    gt = torch.zeros((1, 48), dtype=torch.int64, device=dev)
+    res["pairing_batch_dev_call"], _ = code_of(
+        lambda: ctx.pairing_batch_dev(P.data_ptr(), Q.data_ptr(), n, gt.data_ptr(), st.data_ptr()))
+    torch.cuda.synchronize(dev)
+    res["pairing_batch_dev_status"] = int(st.cpu().item())
+    # the throughput path has no capped waits: the same library must still be right there
+    ctx.set_latency_max(0)
+    ctx.set_fe_wide_max(0)
+    code, v = code_of(lambda: ctx.pairing_many(p, q))
+    res["throughput_path"] = code
+    res["throughput_path_bit_exact"] = bool(v is not None and np.array_equal(v, O.pairing_many(p, q, 8)))
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

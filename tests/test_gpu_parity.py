@@ -268,7 +268,7 @@ def test_throughput_path_pairing_many(ctx_tp, pairs):
 
 
 def test_throughput_path_zero_points(ctx_tp, pairs):
-    """pairing() of a zero point is Fq12::one() (mod.rs:896), on k_pairing_fused / k_fe_out."""
+    """pairing() of a zero point is Fq12::one() (mod.rs:896), on k_pairing_full (a.skip)."""
     p, q = pairs
     p2, q2 = p[:4].copy(), q[:4].copy()
     one = O.canon_to_mont_array([1])
