@@ -317,42 +317,74 @@ constexpr int kRegionResult = 4;           // the final product (element 0, stri
 constexpr size_t kWideGroups = kBlock / 16;  // k_fq12_reduce_wide: 16-lane groups per block
 constexpr size_t kReduceBlocksMax = 512;      // one round of 256-thread blocks, two per CU (kernels_reduce.hip)
 
-// Multiply each of `sets` sets of n split-layout values together on the wide
-// layout (k_fq12_reduce_wide, all sets in one launch per level): set y is
-// elements y * in_set + [0, n) of `in` (stride in_stride), its product goes to
+// sets y < `sets` of n elements each at y * n
+static SetSpan uniform_span(int sets, size_t n) {
+    SetSpan sp{};
+    sp.sets = sets;
+    for (int y = 0; y < sets; ++y) {
+        sp.off[y] = (uint32_t)(y * n);
+        sp.n[y] = (uint32_t)n;
+    }
+    return sp;
+}
+// Multiply each of `sets` (<= kMaxSeg) sets of split-layout values together on
+// the wide layout (k_fq12_reduce_wide, all sets in one launch per level): set y
+// is elements span.off[y] + [0, span.n[y]) of `in` (stride in_stride), its product goes to
 // element out_base + y * out_set of `out` (stride out_stride).  `in` must not
-// be a ping-pong region.  Each level's chain length per group G is the smallest
+// be a ping-pong region.  Each set takes its own number of blocks (one flat grid),
+// so sets of different sizes (the per-segment K of batch_plan) need no padding.
+// Each level's chain length per group G is the smallest
 // power of two >= 2 that needs at most 512 blocks: config 5's 16 x 4,096
 // segment values take two launches (G = 8, then 2) instead of three of G = 2 --
 // 2.20 against 2.25-2.26 ms per product; G = 16 2.21-2.27, G = 32 2.27-2.30
 // (profiles/r4e_ab_reduce.txt, one block per CU then); with two blocks per CU
 // (kernels_reduce.hip) G = 8 stays ahead of G = 4 (profiles/r4q_ab_reduce_lds.txt).
-int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, size_t n, size_t in_set, int sets, uint32_t* out,
+int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, SetSpan span, int sets, uint32_t* out,
                  size_t out_stride, size_t out_base, size_t out_set, hipStream_t s) {
+    if (sets < 1 || sets > kMaxSeg) return fail(c, BN_ERR_INTERNAL, "product reduction: bad set count");
+    span.sets = sets;
     const uint32_t* src = in;
-    size_t sn = n, sstride = in_stride, sset = in_set;
+    size_t sstride = in_stride;
     bool a = true;
     for (;;) {
+        // G (per_group): the smallest power of two >= 2 with at most kReduceBlocksMax
+        // blocks over all sets, each set taking ceil(n[y] / (16 G)) blocks
+        auto blocks_for = [&](int pg) {
+            size_t t = 0;
+            for (int y = 0; y < sets; ++y) t += (span.n[y] + kWideGroups * pg - 1) / (kWideGroups * pg);
+            return t;
+        };
         int per_group = 2;
-        while (per_group < 64 && (size_t)sets * ((sn + kWideGroups * per_group - 1) / (kWideGroups * per_group)) >
-                                     kReduceBlocksMax)
-            per_group *= 2;
+        while (per_group < 64 && blocks_for(per_group) > kReduceBlocksMax) per_group *= 2;
         const size_t per_block = kWideGroups * (size_t)per_group;
-        const size_t blocks = (sn + per_block - 1) / per_block;
-        if (blocks == 1) {
-            k_fq12_reduce_wide<<<dim3(1, sets), kBlock, 0, s>>>(src, sstride, sn, sset, out, out_stride, out_base,
-                                                                out_set, per_group);
+        size_t bmax = 0;
+        span.blk[0] = 0;
+        for (int y = 0; y < sets; ++y) {
+            const size_t by = std::max<size_t>(1, (span.n[y] + per_block - 1) / per_block);  // an empty set: one
+            span.blk[y + 1] = span.blk[y] + (uint32_t)by;
+            bmax = std::max(bmax, by);
+        }
+        const unsigned grid = span.blk[sets];
+        if (bmax == 1) {
+            k_fq12_reduce_wide<<<grid, kBlock, 0, s>>>(src, sstride, span, out, out_stride, out_base, out_set,
+                                                       per_group);
             HIPCHK(c, hipGetLastError());
             return BN_OK;
         }
         uint32_t* dst = slot_region(c, a ? kRegionA : kRegionB);
-        k_fq12_reduce_wide<<<dim3((unsigned)blocks, sets), kBlock, 0, s>>>(src, sstride, sn, sset, dst,
-                                                                            sets * blocks, 0, blocks, per_group);
+        if ((size_t)sets * bmax > c->cap) return fail(c, BN_ERR_INTERNAL, "product reduction exceeds the workspace");
+        k_fq12_reduce_wide<<<grid, kBlock, 0, s>>>(src, sstride, span, dst, sets * bmax, 0, bmax, per_group);
         HIPCHK(c, hipGetLastError());
+        // next level: set y holds its blocks' products at y * bmax (stride sets * bmax)
+        SetSpan nx{};
+        nx.sets = sets;
+        for (int y = 0; y < sets; ++y) {
+            nx.off[y] = (uint32_t)(y * bmax);
+            nx.n[y] = span.blk[y + 1] - span.blk[y];
+        }
+        span = nx;
         src = dst;
-        sstride = sets * blocks;
-        sn = blocks;
-        sset = blocks;
+        sstride = sets * bmax;
         a = !a;
     }
 }
@@ -375,15 +407,30 @@ int run_fe(bn_ctx* c, const uint32_t* f, size_t n, const uint8_t* flags, bn_gt* 
 }
 
 // ---- pairing_batch / miller_loop_batch: segmented Miller loop + device reduction
-constexpr int kRegionSeg = 8;  // k_miller_seg output: S * n elements from region kRegionSeg on
+constexpr int kRegionSeg = 8;  // k_miller_seg output: plan.total elements from region kRegionSeg on
 
-// cut the 64 digits into S segments of about equal work for K pairs per lane
-// pair (a digit: one squaring, 36 Fq-mul, and K lines of 39; a nonzero digit K
-// more lines; the last segment the 2 K closing lines)
+// Work of one lane pair in segment [d, e) of the 64 digits with K pairs: a
+// squaring per digit but the first (36 Fq-mul) and K lines per line of a pair
+// (39 each; two at a nonzero digit, and the last segment's two closing lines).
+static int seg_sq(int d, int e) { return e - d - 1; }
+static int seg_lines(int d, int e) {
+    int L = e == BN_NAF_DIGITS ? 2 : 0;
+    for (int i = d; i < e; ++i) L += 1 + (int)((kNafNonzero >> i) & 1u);
+    return L;
+}
+// (weights from the ISA -- 5,338 VALU per squaring against 4,730 plus the loads per
+// line -- and three settings between them planned no better on the GPU,
+// profiles/r5e_ab_segment_plan.txt)
+constexpr int kSegWSq = 36, kSegWLine = 39;
+static int seg_cost(int d, int e, int K) { return kSegWSq * seg_sq(d, e) + kSegWLine * K * seg_lines(d, e); }
+static void plan_index(SegPlan& p) {
+    for (int k = 0; k < p.S; ++k)
+        p.idx[k] = p.lo[k] + __builtin_popcountll(kNafNonzero & ((p.lo[k] ? (1ull << p.lo[k]) : 1ull) - 1ull));
+}
+// cut the 64 digits into S segments of about equal work for K pairs per lane pair
 static SegPlan cut_plan(int S, int K) {
     SegPlan p{};
     p.S = S;
-    p.K = K;
     auto cost = [K](int d) { return 36 + 39 * K + (((kNafNonzero >> d) & 1u) ? 39 * K : 0); };
     int total = 2 * 39 * K;
     for (int d = 0; d < BN_NAF_DIGITS; ++d) total += cost(d);
@@ -398,29 +445,105 @@ static SegPlan cut_plan(int S, int K) {
     }
     p.hi[g] = BN_NAF_DIGITS;
     p.S = g + 1;
-    for (int k = 0; k < p.S; ++k)
-        p.idx[k] = p.lo[k] + __builtin_popcountll(kNafNonzero & ((p.lo[k] ? (1ull << p.lo[k]) : 1ull) - 1ull));
+    for (int k = 0; k < p.S; ++k) p.K[k] = K;
+    plan_index(p);
+    return p;
+}
+// the lane-pair layout of a plan over n pairs: segment s gets G[s] = ceil(n / K[s])
+// lane pairs from off[s] on, each range rounded up to `align` lane pairs
+static SegPlan plan_layout(SegPlan p, size_t n, uint32_t align) {
+    uint32_t off = 0;
+    for (int k = 0; k < p.S; ++k) {
+        p.G[k] = (uint32_t)((n + (size_t)p.K[k] - 1) / (size_t)p.K[k]);
+        p.off[k] = off;
+        off += (p.G[k] + align - 1) / align * align;
+    }
+    p.total = off;
     return p;
 }
 // pairing_many's latency path: one pair per lane pair (K = 1); S doubles while
 // S*n lane pairs leave the GPU underfilled; 16 segments only for the smallest
 // batches (profiles/r2ac_latency_seg16.txt: 16 helps up to ~1024 pairs, costs
-// at 4096 through the longer Horner recombination of every pair)
+// at 4096 through the longer Horner recombination of every pair).  Unpadded:
+// element s * n + e (k_horner_wide's layout).
 SegPlan seg_plan(size_t n) {
     int S = 1;
     while (S < kMaxSeg && (size_t)S * n < ((size_t)1 << 16) && !(S >= 8 && (size_t)S * n >= ((size_t)1 << 14))) S *= 2;
-    return cut_plan(S, 1);
+    return plan_layout(cut_plan(S, 1), n, 1);
 }
-// pairing_batch / miller_loop_batch (one Horner recombination for the whole
-// product): 16 segments, and K pairs per lane pair sharing one squaring per
-// digit (mod.rs:609-640) -- the largest K <= 16 that still leaves 16 * ceil(n/K)
-// >= 2^16 lane pairs (two waves per SIMD).  At 2^14 terms: K = 4, a lane pair
-// runs 4 digits with one squaring and ~5.3 lines each instead of 16 digits
-// with one squaring and ~1.3 lines each (S = 4, K = 1 before).
+// pairing_batch / miller_loop_batch (one recombination for the whole product):
+// up to 16 digit segments, each with its own number K[s] of pairs per lane pair
+// sharing one squaring per digit (mod.rs:609-640).  The lane-pair budget is the
+// uniform plan's: 16 ceil(n / K0) with K0 the largest power of two <= 16 that
+// still leaves at least 2^16 lane pairs (two waves per SIMD; K0 = 4 at 2^14 terms).
+// Within it the digits and the K[s] minimize the largest segment's work (the
+// kernel runs as long as its heaviest lane pair): a dynamic program over the
+// digit boundaries for a target work T, each segment taking the largest K that
+// keeps it within T, binary-searched on T.  At 2^14 terms: 1,008 against the
+// uniform plan's 1,236 (K = 4 everywhere: 696 to 1,236 per segment).  Each
+// segment's lane pairs are padded to whole 512-thread blocks (256 lane pairs).
 SegPlan batch_plan(size_t n) {
-    int K = 1;
-    while (K < 16 && (size_t)kMaxSeg * ((n + 2 * K - 1) / (2 * K)) >= ((size_t)1 << 16)) K *= 2;
-    return cut_plan(kMaxSeg, K);
+    int K0 = 1;
+    while (K0 < 16 && (size_t)kMaxSeg * ((n + 2 * K0 - 1) / (2 * K0)) >= ((size_t)1 << 16)) K0 *= 2;
+    const size_t align = kPairBlock / kPathLanes;
+    auto padded = [&](int K) { return ((n + (size_t)K - 1) / (size_t)K + align - 1) / align * align; };
+    const size_t budget = (size_t)kMaxSeg * padded(K0);
+    constexpr int D = BN_NAF_DIGITS;
+    constexpr size_t kInf = ~(size_t)0;
+    // dp[e][k]: fewest lane pairs covering digits [0, e) with k segments of work <= T
+    auto solve = [&](int T, SegPlan* out) {
+        static thread_local size_t dp[D + 1][kMaxSeg + 1];
+        static thread_local int from[D + 1][kMaxSeg + 1], kof[D + 1][kMaxSeg + 1];
+        for (auto& r : dp)
+            for (auto& v : r) v = kInf;
+        dp[0][0] = 0;
+        for (int d = 0; d < D; ++d)
+            for (int k = 0; k < kMaxSeg; ++k) {
+                if (dp[d][k] == kInf) continue;
+                for (int e = d + 1; e <= D; ++e) {
+                    const int sq = seg_sq(d, e), L = seg_lines(d, e);
+                    if (kSegWSq * sq + kSegWLine * L > T) break;  // even K = 1 is over T (and grows with e)
+                    int K = (T - kSegWSq * sq) / (kSegWLine * L);
+                    if (K > 64) K = 64;
+                    const size_t v = dp[d][k] + padded(K);
+                    if (v < dp[e][k + 1]) {
+                        dp[e][k + 1] = v;
+                        from[e][k + 1] = d;
+                        kof[e][k + 1] = K;
+                    }
+                }
+            }
+        int best = -1;
+        for (int k = 1; k <= kMaxSeg; ++k)
+            if (dp[D][k] <= budget && (best < 0 || dp[D][k] < dp[D][best])) best = k;
+        if (best < 0) return false;
+        if (out) {
+            SegPlan p{};
+            p.S = best;
+            for (int e = D, k = best; k > 0; --k) {
+                const int d = from[e][k];
+                p.lo[k - 1] = d;
+                p.hi[k - 1] = e;
+                p.K[k - 1] = kof[e][k];
+                e = d;
+            }
+            plan_index(p);
+            *out = p;
+        }
+        return true;
+    };
+    SegPlan uni = cut_plan(kMaxSeg, K0);
+    int hi = 0;
+    for (int k = 0; k < uni.S; ++k) hi = std::max(hi, seg_cost(uni.lo[k], uni.hi[k], K0));
+    int lo = 1;
+    if (!solve(hi, nullptr)) return plan_layout(uni, n, (uint32_t)align);
+    while (lo < hi) {
+        const int mid = (lo + hi) / 2;
+        if (solve(mid, nullptr)) hi = mid; else lo = mid + 1;
+    }
+    SegPlan p{};
+    solve(hi, &p);
+    return plan_layout(p, n, (uint32_t)align);
 }
 
 // Segment values of m <= kChunk device pairs (mode 0: a pair with a zero point
@@ -430,12 +553,19 @@ SegPlan batch_plan(size_t n) {
 int chunk_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int mode, const SegPlan& plan,
                   uint32_t* parts, size_t nchunks, size_t k, hipStream_t s) {
     RET_IF(prepare(c, d_p, d_q, m, mode, s));
-    const size_t G = (m + plan.K - 1) / plan.K;  // lane-pair groups per segment
-    k_miller_seg<<<grid_pair(kPathLanes * plan.S * G), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
-                                                                       slot_region(c, kRegionSeg));
+    const SegPlan lay = plan_layout(plan, m, kPairBlock / kPathLanes);  // this chunk's lane pairs
+    // k_miller_seg writes lay.total elements from region kRegionSeg to the end of the slots
+    if ((size_t)lay.total > (size_t)(kFeSlots - kRegionSeg) * c->cap)
+        return fail(c, BN_ERR_INTERNAL, "segment layout exceeds the workspace");
+    k_miller_seg<<<grid_pair(kPathLanes * (size_t)lay.total), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, lay,
+                                                                              slot_region(c, kRegionSeg));
     HIPCHK(c, hipGetLastError());
-    return product_wide(c, slot_region(c, kRegionSeg), plan.S * G, G, G, plan.S, parts, plan.S * nchunks, k, nchunks,
-                        s);
+    SetSpan sp{};
+    for (int k2 = 0; k2 < lay.S; ++k2) {
+        sp.off[k2] = lay.off[k2];
+        sp.n[k2] = lay.G[k2];
+    }
+    return product_wide(c, slot_region(c, kRegionSeg), lay.total, sp, lay.S, parts, plan.S * nchunks, k, nchunks, s);
 }
 // where chunk partials go: straight into the result region (element g, stride S)
 // for one chunk, else the parts region
@@ -463,7 +593,7 @@ static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out
 // recombination (+ the final exponentiation for pairing_batch) into *d_out
 int finish_product(bn_ctx* c, const SegPlan& plan, size_t nchunks, int do_fe, bn_gt* d_out, hipStream_t s) {
     if (nchunks > 1)
-        RET_IF(product_wide(c, slot_region(c, kRegionParts), plan.S * nchunks, nchunks, nchunks, plan.S,
+        RET_IF(product_wide(c, slot_region(c, kRegionParts), plan.S * nchunks, uniform_span(plan.S, nchunks), plan.S,
                             slot_region(c, kRegionResult), plan.S, 0, 1, s));
     return recombine_one(c, plan, do_fe, d_out, s);
 }
@@ -490,7 +620,8 @@ int latency_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int
     RET_IF(reserve(c, n));
     launch_latency(c, d_p, d_q, n, nullptr, slot_region(c, kRegionSeg), mode, s);
     HIPCHK(c, hipGetLastError());
-    RET_IF(product_wide(c, slot_region(c, kRegionSeg), n, n, n, 1, slot_region(c, kRegionResult), 1, 0, 1, s));
+    RET_IF(product_wide(c, slot_region(c, kRegionSeg), n, uniform_span(1, n), 1, slot_region(c, kRegionResult), 1, 0,
+                        1, s));
     return recombine_one(c, cut_plan(1, 1), do_fe, d_out, s);  // one segment: the FE of the product when do_fe
 }
 // (at most one chunk: the one-launch path reserves workspace for all n pairs)
@@ -782,7 +913,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             const SegPlan plan = seg_plan(m);
             RET_IF(prepare(c, d_p + off, d_q + off, m, 0, s));
             mark(1);
-            k_miller_seg<<<grid_pair(kPathLanes * plan.S * m), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
+            k_miller_seg<<<grid_pair(kPathLanes * (size_t)plan.total), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, plan,
                                                                                slot_region(c, kRegionSeg));
             mark(2);
             k_horner_wide<<<wide_blocks(m), kBlock, 0, s>>>(slot_region(c, kRegionSeg), m, plan, 1, d_out + off,
@@ -813,7 +944,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
                                                                   c->d_err, 0);
             mark(1);
             if (c->miller_form == 2) {  // the segment kernel with one segment: the whole loop
-                const SegPlan whole = seg_plan(~(size_t)0 >> 1);
+                const SegPlan whole = plan_layout(cut_plan(1, 1), m, 1);  // one segment: the whole loop
                 k_miller_seg<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(c->coeffs, c->paff, c->flags, m, whole,
                                                                           c->slots);
             } else {

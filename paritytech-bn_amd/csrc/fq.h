@@ -80,6 +80,7 @@ template <int K>
 struct Fq {
     static_assert(kv(K) >= 1 && kv(K) <= kMaxBound, "Fq value bound out of range");
     static_assert(kl(K) >= 1 && kl(K) <= kMaxLimb, "Fq digit bound out of range");
+    static constexpr int kK = K;  // the bound code, for static checks on deduced types
     uint32_t v[9];
 };
 
@@ -206,14 +207,35 @@ BN_INLINE Fq<kv(K)> fq_neg(const Fq<K>& a_in) {
     return fq_norm(Fq<kenc(B, 2)>{{r.v[0], r.v[1], r.v[2], r.v[3], r.v[4], r.v[5], r.v[6], r.v[7], r.v[8]}});
 }
 
+// Sticky device error bits (bn_status codes as bit numbers) of a call: the word
+// is global memory (the context's d_err), so the OR goes through a global-space
+// pointer -- a generic-pointer atomicOr gets an aperture test from the backend,
+// which in kernels_pairing.hip it emitted as an illegal VOPC ("Operand has
+// incorrect register class", V_CMP_NE_U32_e32 0, src_shared_base) as soon as the
+// unit's code changed (the fold-check build in rounds 3-4, the column-sum asm).
+#if defined(__HIPCC__)
+__device__ __forceinline__ void err_or(int* err, int bit) {
+    __hip_atomic_fetch_or((__attribute__((address_space(1))) int*)err, 1 << bit, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
+
 // ---------------------------------------------------------------- single-chain column sums
-// BN_DOT2_ASM (device code): fq_mul, fq_sqr and fq2_split.h fq_dot2 run the
-// hand-scheduled product scan of dot2_asm.inc (tools/gen_dot2_asm.py): one
-// v_mad_u64_u32 chain per product, each column started from the previous
-// column's carry, so no carry-merge instruction per column.  The same column
-// sums in another association order: identical digits.
+// BN_DOT2_ASM (device code, on by default): fq_mul, fq_sqr and fq2_split.h
+// fq_dot2 run the hand-scheduled product scan of dot2_asm.inc
+// (tools/gen_dot2_asm.py): one v_mad_u64_u32 chain per product, each column
+// started from the previous column's carry, so no carry-merge instruction per
+// column (the compiler's schedule starts each column as its own chain and adds
+// the carry with a v_lshl_add_u64: 16 per product, 3,748 in k_pairing_full).  A
+// dependent v_mad_u64_u32 issues as fast as an independent one on gfx950
+// (profiles/r3j_mad_issue.txt).  The same column sums in another association
+// order: identical digits.  Measured (profiles/r5b_ab_dot2_asm.txt, two
+// interleaved rounds): k_pairing_full 7.75 -> 7.60 ms, config 5 2.17 -> 2.08-2.12
+// ms, G2 * Fr 6.19 -> 5.92 ms, config 3 8.11 -> 7.64 ms.  BN_DOT2_ASM=0 builds
+// the compiler's form (host builds always use it).
+// Bits: 1 = fq_dot2, 2 = fq_mul, 4 = fq_sqr.
 #ifndef BN_DOT2_ASM
-#define BN_DOT2_ASM 0
+#define BN_DOT2_ASM 7
 #endif
 #if BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
 #include "dot2_asm.inc"
@@ -296,8 +318,10 @@ BN_INLINE auto fq_mul(const Fq<A>& a_in, const Fq<B>& b_in) {
     const Fq<B>& b = b_in;
     Fq<mul_bound(kv(A), kv(B))> r;
 #if BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
-    asm(BN_ASM_MUL : BN_ASM_OUT9(r.v) : BN_ASM_IN9(a.v), BN_ASM_IN9(b.v), BN_ASM_P : BN_ASM_CLOBBER);
-    return r;
+    if constexpr ((BN_DOT2_ASM & 2) != 0) {
+        asm(BN_ASM_MUL : BN_ASM_OUT9(r.v) : BN_ASM_IN9(a.v), BN_ASM_IN9(b.v), BN_ASM_P : BN_ASM_CLOBBER);
+        return r;
+    }
 #endif
     uint32_t m[9];
     uint64_t acc = 0;
@@ -339,8 +363,10 @@ BN_INLINE auto fq_sqr(const Fq<B>& a_in) {
     for (int i = 0; i < 9; ++i) d[i] = a.v[i] << 1;
     Fq<mul_bound(kv(B), kv(B))> r;
 #if BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
-    asm(BN_ASM_SQR : BN_ASM_OUT9(r.v) : BN_ASM_IN9(a.v), BN_ASM_IN9(d), BN_ASM_P : BN_ASM_CLOBBER);
-    return r;
+    if constexpr ((BN_DOT2_ASM & 4) != 0) {
+        asm(BN_ASM_SQR : BN_ASM_OUT9(r.v) : BN_ASM_IN9(a.v), BN_ASM_IN9(d), BN_ASM_P : BN_ASM_CLOBBER);
+        return r;
+    }
 #endif
     uint32_t m[9];
     uint64_t acc = 0;

@@ -255,40 +255,47 @@ __device__ __forceinline__ Fq<2> w12_from_line(uint32_t ln_off) {
 // computes tmp_e = x*y for pair k = e; lane pair e >= 3 computes
 // (x + y)(xi*y + x) for pair k = e - 3; then every lane forms its output
 // coordinate from them: t0 = P3 - P0 - xi*P0 etc. as in the reference.
+// Operands are chosen by LDS address rather than by per-digit selects: slots
+// 12..15 of A_ (the mirror lanes') hold zero, the "absent" term of the lo lanes,
+// and each lane reads its own and its partner coordinate of V directly; xi * a
+// stays unfolded (bound 21p: the product's column budget and bound allow it)
+// and the product is stored at its own bound 3p.  787 -> 7xx VALU per squaring
+// (profiles/r5e_*).
+__device__ __forceinline__ Fq<21> w_xi_loose(const Fq<2>& a) { return fq_norm(fq2_mul_xi(Fq2<2>{a}).c); }
 __device__ __noinline__ Fq<2> w12_cyc(Fq<2> a) {
     const WL w = wl();
     uint32_t* A_ = w.gb;
     uint32_t* X_ = w.gb + kWArr;
     uint32_t* P_ = w.gb + 2 * kWArr;
     uint32_t* Q_ = w.gb + 3 * kWArr;
-    w_put(A_, w.l, a);
-    w_put(X_, w.l, w_xi(a));
+    constexpr int kZ = 12;  // a zero slot of A_
+    w_put(A_, w.l, fq_select(w.l >= 12, widen<2>(fq_zero()), a));
+    w_put(X_, w.l, w_xi_loose(a));
     w_sync();
     const bool hi = w.e >= 3;
-    const int k = hi ? w.e - 3 : w.e;
-    const Fq<2> x0 = w_get<2>(A_, 2 * k), x1 = w_get<2>(A_, 2 * k + 1);
-    const Fq<2> y0 = w_get<2>(A_, 2 * k + 6), y1 = w_get<2>(A_, 2 * k + 7);
-    const Fq<2> xy0 = w_get<2>(X_, 2 * k + 6), xy1 = w_get<2>(X_, 2 * k + 7);  // xi * y
-    // U = hi ? x + y : x,  V = hi ? xi*y + x : y (V's digits stay lazy: the column
-    // budget of u*vo + u*vx is 1*2 + 1*4 with U normalized)
-    const Fq<4> u0 = fq_norm(fq_pick(hi, fq_add(x0, y0), x0));
-    const Fq<4> u1 = fq_norm(fq_pick(hi, fq_add(x1, y1), x1));
-    const auto v0 = fq_pick(hi, fq_add(xy0, x0), y0);
-    const auto v1 = fq_pick(hi, fq_add(xy1, x1), y1);
-    // lane c of U*V: c0 = u0 v0 - u1 v1, c1 = u0 v1 + u1 v0
-    const auto vo = fq_select(w.c != 0, v1, v0);
-    const auto vx = fq_pick(w.c != 0, v0, fq_neg_lazy(v1));
+    const int k = hi ? w.e - 3 : w.e, c = w.c;
+    // U = hi ? x + y : x;  V = hi ? xi*y + x : y: this lane's coordinate of V and
+    // its partner's, each as (xi*y or y) + (x or zero)
+    const uint32_t* VS = hi ? X_ : A_;
+    const Fq<4> u0 = fq_norm(fq_add(w_get<2>(A_, 2 * k), w_get<2>(A_, hi ? 2 * k + 6 : kZ)));
+    const Fq<4> u1 = fq_norm(fq_add(w_get<2>(A_, 2 * k + 1), w_get<2>(A_, hi ? 2 * k + 7 : kZ)));
+    const auto vo = fq_add(w_get<21>(VS, 2 * k + 6 + c), w_get<2>(A_, hi ? 2 * k + c : kZ));
+    const auto vp = fq_add(w_get<21>(VS, 2 * k + 7 - c), w_get<2>(A_, hi ? 2 * k + 1 - c : kZ));
+    // lane c of U*V: c0 = u0 v0 - u1 v1 (vx = -v1), c1 = u0 v1 + u1 v0 (vx = v0)
+    const auto vx = fq_pick(c != 0, vp, fq_neg_lazy(vp));
     const auto p = fq_dot2(u0, vo, u1, vx);
-    const Fq<2> pn = w_narrow(p);
+    static_assert(kl(decltype(fq_dot2(u0, vo, u1, vx))::kK) == 1 && kv(decltype(fq_dot2(u0, vo, u1, vx))::kK) <= 3,
+                  "w12_cyc: the product is stored as a normalized value <= 3p");
+    const Fq<3> pn = widen<3>(p);
     w_put(P_, w.l, pn);
     w_put(Q_, w.l, w_xi(pn));
     w_sync();
     // even e (z0, z4, z3 = w^0, w^2, w^4): 3*(P_(k+3) - P_k - xi*P_k) - 2*a with k = e/2
     // odd e: z1 = w^3: 6*P_0 + 2a;  z5 = w^5: 6*P_1 + 2a;  z2 = w^1: 6*xi*P_2 + 2a
     const int ka = w.e >> 1;
-    const Fq<2> pu = w_get<2>(P_, 2 * (ka + 3) + w.c), pv = w_get<2>(P_, 2 * ka + w.c);
-    const Fq<2> pw = w_get<2>(Q_, 2 * ka + w.c);
-    const Fq<2> px = w.e == 1 ? w_get<2>(Q_, 4 + w.c) : w_get<2>(P_, (w.e >= 3 ? w.e - 3 : 0) + w.c);
+    const Fq<3> pu = w_get<3>(P_, 2 * (ka + 3) + c), pv = w_get<3>(P_, 2 * ka + c);
+    const Fq<2> pw = w_get<2>(Q_, 2 * ka + c);
+    const Fq<3> px = w.e == 1 ? widen<3>(w_get<2>(Q_, 4 + c)) : w_get<3>(P_, (w.e >= 3 ? w.e - 3 : 0) + c);
     // one stream for both parities: 3*T + (-2a | 2a), T = ta (even e) or 2*px (odd e)
     const bool even = (w.e & 1) == 0;
     const auto ta = fq_norm(fq_sub(fq_sub(pu, pv), pw));
@@ -501,7 +508,7 @@ __device__ __forceinline__ void duo_wait(const volatile uint32_t* c, uint32_t v,
         for (; *c < v && spins < kDuoSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
     if (*c < v) {
         dead = true;
-        if (err) atomicOr(err, 1 << BN_ERR_INTERNAL);
+        if (err) err_or(err, BN_ERR_INTERNAL);
     }
     asm volatile("" ::: "memory");
 }

@@ -173,9 +173,11 @@ BN_INLINE auto fq_dot2(const Fq<X>& x, const Fq<Y>& y, const Fq<Z>& z, const Fq<
     constexpr int BO = 1 + (int)(((long long)kv(X) * kv(Y) + (long long)kv(Z) * kv(W)) * 5908 / 1000000 + 1);
     Fq<BO> r;
 #if BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
-    asm(BN_ASM_DOT2 : BN_ASM_OUT9(r.v) : BN_ASM_IN9(x.v), BN_ASM_IN9(y.v), BN_ASM_IN9(z.v), BN_ASM_IN9(w.v), BN_ASM_P
-        : BN_ASM_CLOBBER);
-    return r;
+    if constexpr ((BN_DOT2_ASM & 1) != 0) {
+        asm(BN_ASM_DOT2 : BN_ASM_OUT9(r.v) : BN_ASM_IN9(x.v), BN_ASM_IN9(y.v), BN_ASM_IN9(z.v), BN_ASM_IN9(w.v), BN_ASM_P
+            : BN_ASM_CLOBBER);
+        return r;
+    }
 #endif
     uint32_t m[9];
     uint64_t acc = 0;

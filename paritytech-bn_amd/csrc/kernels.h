@@ -431,13 +431,21 @@ __device__ __forceinline__ Balance balance_init() {
 // `pos`: this wave's position in the (shared) program, non-decreasing.  The
 // priority is the number of other waves on the SIMD not behind this one (a tie
 // counts: two tied waves both run at 1, and age decides between them).
+// The position words are read and written as relaxed workgroup-scope atomics:
+// they become plain LDS operations (ds_read / ds_write).  Through a volatile
+// generic pointer they were flat_load/flat_store sc0 sc1 (rounds 3-4), and in
+// k_pairing_full the backend then emitted an illegal VOPC for the LDS-to-flat
+// cast as soon as the unit's code changed ("Operand has incorrect register
+// class", V_CMP_NE_U32_e32 0, src_shared_base).
+__device__ __forceinline__ uint32_t bal_ld(uint32_t j) {
+    return __hip_atomic_load(&g_bal_prog[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ void balance_step(const Balance& b, uint32_t pos) {
-    volatile uint32_t* pr = g_bal_prog;
-    pr[b.w] = pos;
-    uint32_t ahead = __builtin_amdgcn_readfirstlane(pr[b.partner]) >= pos && b.partner != b.w ? 1u : 0u;
+    __hip_atomic_store(&g_bal_prog[b.w], pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint32_t ahead = __builtin_amdgcn_readfirstlane(bal_ld(b.partner)) >= pos && b.partner != b.w ? 1u : 0u;
     if (b.more) {
         for (uint32_t m = b.more; m; m &= m - 1)
-            ahead += __builtin_amdgcn_readfirstlane(pr[__builtin_ctz(m)]) >= pos ? 1u : 0u;
+            ahead += __builtin_amdgcn_readfirstlane(bal_ld(__builtin_ctz(m))) >= pos ? 1u : 0u;
         if (ahead >= 3) __builtin_amdgcn_s_setprio(3);
         else if (ahead == 2) __builtin_amdgcn_s_setprio(2);
     }
@@ -494,14 +502,25 @@ inline void vm_step(uint32_t out[2], uint32_t op, uint32_t d, uint32_t a, uint32
 // Segments of the Miller loop's 64 NAF digits (k_miller_seg / k_horner_wide):
 // segment s covers digits [lo[s], hi[s]) and starts at line coefficient idx[s]
 constexpr int kMaxSeg = 16;
-// K: pairs per lane pair -- the reference's shared-squaring multi-Miller loop
-// (mod.rs:609-640): lane pair g of a segment squares its accumulator once per
-// digit and multiplies in the lines of pairs g, g + G, ..., g + (K-1) G
-// (G = ceil(n / K)); K = 1 for pairing_many's per-pair loops
+// K[s]: pairs per lane pair of segment s -- the reference's shared-squaring
+// multi-Miller loop (mod.rs:609-640): lane pair g of segment s squares its
+// accumulator once per digit and multiplies in the lines of pairs g, g + G[s],
+// ..., g + (K[s]-1) G[s] (G[s] = ceil(n / K[s])); K = 1 for pairing_many's
+// per-pair loops.  Segment s's lane pairs are [off[s], off[s] + G[s]) of `total`
+// (k_miller_seg writes element off[s] + g); a pairing_batch plan pads each
+// segment's range to whole 512-thread blocks, so no block mixes two segments.
 struct SegPlan {
     int S;
-    int K;
     int lo[kMaxSeg], hi[kMaxSeg], idx[kMaxSeg];
+    int K[kMaxSeg];
+    uint32_t G[kMaxSeg], off[kMaxSeg], total;
+};
+// the element ranges of the sets k_fq12_reduce_wide multiplies (set y: elements
+// off[y] .. off[y] + n[y] - 1 of its input) and the blocks that take them (set y:
+// blocks blk[y] .. blk[y + 1] - 1 of the launch, one output element each)
+struct SetSpan {
+    uint32_t off[kMaxSeg], n[kMaxSeg], blk[kMaxSeg + 1];
+    int sets;
 };
 
 // ---------------------------------------------------------------- kernels
@@ -547,7 +566,7 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
                                                     bn_gt* __restrict__ out, uint8_t* __restrict__ ok,
                                                     int* __restrict__ err, int duo);
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
-                                                             size_t n, size_t in_set, uint32_t* __restrict__ out,
+                                                             SetSpan sets, uint32_t* __restrict__ out,
                                                              size_t out_stride, size_t out_base, size_t out_set, int per_group);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
 // (a producer wave for the lines, consumer groups for the wide Miller loop + FE)

@@ -44,7 +44,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_fe_out(const uint32_t* 
     const bool zero = !skip && fq12_is_zero(ld_fq12<kF>(slots, nl, i));
     if (ok && lead) ok[e] = zero ? 0 : 1;
     if (zero) {
-        if (err && lead) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        if (err && lead) err_or(err, BN_ERR_FE_ZERO);
         st_gt_zero(out[e]);
     } else if (skip) {
         st_gt(out[e], fq12_one());

@@ -146,7 +146,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_pairing_full(const 
     st_fq12(slots, nl, l, f);
     const Fq12<kF> r = fq12_vm_run(prog, nsteps, slots, nl, l, bal, 1u << 20, false);
     if (zero) {
-        if ((l % kL) == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        if ((l % kL) == 0) err_or(err, BN_ERR_FE_ZERO);
         st_gt_zero(out[i]);
     } else if (a.skip) {
         st_gt(out[i], fq12_one());
@@ -173,14 +173,16 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* 
 }
 
 // Miller loop in segments (pairing_batch / miller_loop_batch, and small
-// pairing_many batches): lane pair (segment s, group g) -- segment-major, so a
-// wave reads consecutive pairs' coefficients -- runs the segment's digits
-// [lo, hi) of the loop from f = one for the K pairs g, g + G, ..., g + (K-1) G
-// (G = ceil(n / K)): per digit ONE squaring of the shared accumulator and the
-// line of every pair (mod.rs:609-640's shared-squaring loop; squaring is a ring
-// homomorphism and Fq12 is commutative, so the product over groups and the
-// Horner recombination over segments give exactly miller_loop_batch's value).
-// The result goes to element s * G + g of `out` (split layout, stride S * G).
+// pairing_many batches): lane pair off[s] + g (segment s, group g) --
+// segment-major, so a wave reads consecutive pairs' coefficients -- runs the
+// segment's digits [lo, hi) of the loop from f = one for the K[s] pairs g, g + G,
+// ..., g + (K[s]-1) G (G = G[s] = ceil(n / K[s])): per digit ONE squaring of the
+// shared accumulator and the line of every pair (mod.rs:609-640's
+// shared-squaring loop; squaring is a ring homomorphism and Fq12 is commutative,
+// so the product over groups and the Horner recombination over segments give
+// exactly miller_loop_batch's value).  The result goes to element off[s] + g of
+// `out` (split layout, stride total); lane pairs past G[s] (a segment's padding
+// to whole blocks) write nothing.
 // A pair with a zero point (flags) or past n contributes the line one
 // (ell_0 = 1, ell_vw = ell_vv = 0): the sparse product by it is f itself.
 // Launched with kPairBlock threads per block (kernels.h: issue balance).
@@ -191,10 +193,12 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
     fold_table_init();
     const Balance bal = balance_init();
     const size_t l = lane_id(), lp = l / kL, nl = kL * n;
-    const size_t K = (size_t)plan.K, G = (n + K - 1) / K;
-    if (lp >= (size_t)plan.S * G) return;
-    const int s = (int)(lp / G);
-    const size_t g = lp % G, c = l % kL;
+    if (lp >= (size_t)plan.total) return;
+    int s = 0;
+    while (s + 1 < plan.S && lp >= (size_t)plan.off[s + 1]) ++s;
+    const size_t K = (size_t)plan.K[s], G = plan.G[s];
+    const size_t g = lp - plan.off[s], c = l % kL;
+    if (g >= G) return;
     const Ell one_line = {widen<kLine>(fq2_one()), widen<kLine>(fq2_zero()), widen<kLine>(fq2_zero())};
     // line k of pair t of this group, with the pair's affine P
     struct PairLine {
@@ -240,7 +244,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
             }
         }
     }
-    st_fq12(out, kL * plan.S * G, l, f);
+    st_fq12(out, kL * (size_t)plan.total, l, f);
 }
 
 // G2 * Fr (mod.rs:272-292) on the pairing path's two-lane layout: the chain of

@@ -13,16 +13,18 @@
 
 namespace bn {
 
-// Product reduction of several independent sets (blockIdx.y = set y, the
-// elements y * in_set + [0, n) of `in`, split layout, stride in_stride): block
-// (b, y) multiplies the set's elements [16Gb, 16Gb + 16G) (G = per_group) -- a
+// Product reduction of several independent sets (set y: the elements
+// sets.off[y] + [0, sets.n[y]) of `in`, split layout, stride in_stride, taken by
+// the blocks sets.blk[y] .. sets.blk[y + 1] - 1, so sets of different sizes need
+// no padding blocks): block b of set y multiplies the set's elements
+// [16Gb, 16Gb + 16G) (G = per_group) -- a
 // chain of G factors per group (elements g, g + 16, ...), then a tree over the 16
 // groups through LDS -- and writes the block's product as element out_base + y *
-// out_set + b of `out` (stride out_stride).  Elements past n count as one.  The
+// out_set + b of `out` (stride out_stride).  Elements past n[y] count as one.  The
 // order of the factors differs from the reference's left-to-right accumulation;
 // Fq12 multiplication is commutative and associative, so the value is the same.
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
-                                                             size_t n, size_t in_set, uint32_t* __restrict__ out,
+                                                             SetSpan sets, uint32_t* __restrict__ out,
                                                              size_t out_stride, size_t out_base, size_t out_set,
                                                              int per_group) {
     fold_table_init();
@@ -32,7 +34,11 @@ __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __r
     // a chain -- at each step the block's 16 groups read 16 consecutive elements --
     // with the next factor's load issued before the product that precedes it
     // (factors past n are skipped), then the groups' values meet in the tree below
-    const size_t e0 = (size_t)blockIdx.x * kWGroups * (size_t)per_group + g, sb = (size_t)blockIdx.y * in_set;
+    int set = 0;
+    while (set + 1 < sets.sets && blockIdx.x >= sets.blk[set + 1]) ++set;  // block-uniform
+    const size_t b = blockIdx.x - sets.blk[set];
+    const size_t e0 = b * kWGroups * (size_t)per_group + g, sb = sets.off[set];
+    const size_t n = sets.n[set];
     const Fq<2> one = fq_select(w.e == 0 && w.c == 0, widen<2>(fq_one()), widen<2>(fq_zero()));
     Fq<2> x = e0 < n ? w_ld_split(in, in_stride, sb + e0, w) : one;
     Fq<2> y = e0 + kWGroups < n ? w_ld_split(in, in_stride, sb + e0 + kWGroups, w) : one;
@@ -57,7 +63,7 @@ __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __r
         }
         __syncthreads();
     }
-    if (g == 0) w_st_split(out, out_stride, out_base + blockIdx.y * out_set + blockIdx.x, w, x);
+    if (g == 0) w_st_split(out, out_stride, out_base + (size_t)set * out_set + b, w, x);
 }
 
 }  // namespace bn

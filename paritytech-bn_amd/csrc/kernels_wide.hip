@@ -108,7 +108,7 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
     const Fq<2> x = w_ld_split(f, stride, e, w);
     const bool zero = w12_is_zero(x);
     if (ok && w.l == 0 && live) ok[e] = zero ? 0 : 1;
-    if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+    if (zero && err && w.l == 0 && live) err_or(err, BN_ERR_FE_ZERO);
     const Fq<2> r = w_final_exp(role, x, err);
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!zero) fq_store_ref(r, words);
@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_wide(const uint32_t* __restri
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (do_fe) {
         const bool zero = w12_is_zero(x);
-        if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        if (zero && err && w.l == 0 && live) err_or(err, BN_ERR_FE_ZERO);
         const Fq<2> r = w_final_exp(role, x, err);
         HOR_STAMP(5);  // final exponentiation done
         if (!zero) fq_store_ref(r, words);
@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restri
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (do_fe) {
         const bool zero = g_hor_zero != 0;
-        if (zero && err && w.l == 0 && grp == 0) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+        if (zero && err && w.l == 0 && grp == 0) err_or(err, BN_ERR_FE_ZERO);
         const Fq<2> r = w_fe_last(role, x, err);
         HOR_STAMP(5);  // final exponentiation done
         if (!zero) fq_store_ref(r, words);

@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
                     __builtin_amdgcn_s_sleep(1);
             if (BN_ANY(valid && line - (int)cons[j] >= kLatRing)) {  // ring overrun: fail the call
                 dead = true;  // sticky for the wave: no later wait spins again
-                if (L == 0 && err) atomicOr(err, 1 << BN_ERR_INTERNAL);
+                if (L == 0 && err) err_or(err, BN_ERR_INTERNAL);
             }
             asm volatile("" ::: "memory");
             if (st) {  // the operand forms c0, c1, -c1 of each coefficient (fq12_wide.h w12_mul_line)
@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
             for (; prod[j] <= (uint32_t)line && spins < kLatSpinCap; ++spins) __builtin_amdgcn_s_sleep(1);
         if (prod[j] <= (uint32_t)line) {  // line never published: fail the call
             dead = true;
-            if (w.l == 0 && err) atomicOr(err, 1 << BN_ERR_INTERNAL);
+            if (w.l == 0 && err) err_or(err, BN_ERR_INTERNAL);
         }
         asm volatile("" ::: "memory");
     };
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
         return;
     }
     const bool zero = w12_is_zero(x);
-    if (zero && err && w.l == 0 && live) atomicOr(err, 1 << BN_ERR_FE_ZERO);
+    if (zero && err && w.l == 0 && live) err_or(err, BN_ERR_FE_ZERO);
 #if BN_FE_DUO
     WDuo duo = {g_lat_ring + j * kLatRing * kLatLineWords, g_lat_duo + 4 * j, 0, 0, err};
     const Fq<2> res = w12_final_exp_s(x, duo);

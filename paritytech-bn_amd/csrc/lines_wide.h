@@ -43,7 +43,7 @@ __device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p
     const Fq2<2> qz = {fq_load_ref(w0), fq_load_ref(w1)};
     const auto nq = fq_add(fq_sqr(qz.c0), fq_sqr(qz.c1));
 #endif
-    if ((p_zero || q_zero) && mode == 1 && (l % kL) == 0) atomicOr(err, 1 << BN_ERR_TO_AFFINE);
+    if ((p_zero || q_zero) && mode == 1 && (l % kL) == 0) err_or(err, BN_ERR_TO_AFFINE);
     if (flags) flags[l] = (p_zero || q_zero) ? 1 : 0;
 
     // One inversion for both points (Montgomery's trick): t = (pz * N(qz))^-1 with

@@ -1,11 +1,11 @@
 #!/bin/bash
 # Build an A/B variant of libbn254mi.so with extra compile flags into
-# exp/lib_NAME.so (bench.py / tests load it with BN254MI_LIB=exp/lib_NAME.so).
+# exp/lib_NAME.so (bench.py / tests load it with BN254MI_LIB=ab/lib_NAME.so).
 # Usage: tools/build_variant.sh NAME "-DFLAG=1 ..."
 set -e
 NAME=$1; FLAGS=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-B=$ROOT/exp/build_$NAME
+B=$ROOT/ab/build_$NAME
 mkdir -p $B
 SRCS="kernels_pairing kernels_fe kernels_group kernels_util kernels_codec kernels_gtpow kernels_wide kernels_latency_w2 kernels_reduce capi capi_multi"
 for s in $SRCS; do
@@ -13,5 +13,5 @@ for s in $SRCS; do
     -c -o $B/$s.o $ROOT/paritytech-bn_amd/csrc/$s.hip &
 done
 wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $ROOT/exp/lib_$NAME.so $(for s in $SRCS; do echo $B/$s.o; done) -ldl
-echo "built exp/lib_$NAME.so"
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $ROOT/ab/lib_$NAME.so $(for s in $SRCS; do echo $B/$s.o; done) -ldl
+echo "built ab/lib_$NAME.so"
