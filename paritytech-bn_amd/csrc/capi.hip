@@ -579,8 +579,10 @@ uint32_t* parts_region(bn_ctx* c, size_t nchunks) {
 // rule), kept for A/B
 static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out, hipStream_t s) {
     const char* env = getenv("BN254MI_HORNER_TREE");
-    const bool tree = !(env && env[0] == '0');
-    if (tree)
+    const int tree = env ? atoi(env) : 2;  // 2: k_horner_tree2 (default), 1: k_horner_tree, 0: k_horner_wide
+    if (tree == 2 && BN_FE_DUO && plan.S <= kMaxSeg)
+        k_horner_tree2<<<1, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err);
+    else if (tree != 0)
         k_horner_tree<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err,
                                            wide_duo(1) ? 1 : 0);
     else

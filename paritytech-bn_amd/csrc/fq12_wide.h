@@ -38,7 +38,12 @@ constexpr int kWArr = kWLanes * kWSlot;             // words of one operand arra
 #endif
 constexpr int kWArrs = BN_WIDE_ARRS;
 constexpr int kWGroupWords = kWArrs * kWArr;        // 3.75 KB per group
-constexpr int kWGroups = kBlock / kWLanes;          // 16 groups per 256-thread block
+// threads of the blocks of the including translation unit's wide kernels (256:
+// 16 groups)
+#ifndef BN_WIDE_THREADS
+#define BN_WIDE_THREADS kBlock
+#endif
+constexpr int kWGroups = BN_WIDE_THREADS / kWLanes;  // 16 groups per 256-thread block
 __shared__ uint32_t g_wide[kWGroups * kWGroupWords];  // 60 KB
 
 // this lane's place in its group
@@ -305,6 +310,60 @@ __device__ __noinline__ Fq<2> w12_cyc(Fq<2> a) {
     return fq_fold(fq_add(fq_add(t, fq_add(t, t)), s));
 }
 
+// The same squaring on a PAIR of groups of one wave (lanes 32j..32j+15: the main
+// group, 32j+16..32j+31: the helper), both holding the element: kernels_tail.hip's
+// squarer.  The helper's lo lanes compute xi * P_k = (xi x_k) * y_k (xi * x_k is in
+// its X_ array already) while the main group computes P_k, so the xi * P values
+// the output needs come with the products instead of a w_xi pass after them (~95
+// VALU and one LDS round trip fewer per squaring on the chain); both groups then
+// form every output coordinate from the main group's P_ and the helper's.  The
+// values are the reference's: xi * (x y) and (xi x) y are the same field element.
+__device__ __noinline__ Fq<2> w12_cyc32(Fq<2> a) {
+    const WL w = wl();
+    const bool helper = (((int)threadIdx.x / kWLanes) & 1) != 0;
+    uint32_t* A_ = w.gb;
+    uint32_t* X_ = w.gb + kWArr;
+    uint32_t* P_ = w.gb + 2 * kWArr;
+    const uint32_t* PM = (helper ? w.gb - kWGroupWords : w.gb) + 2 * kWArr;  // the main group's products
+    const uint32_t* PH = (helper ? w.gb : w.gb + kWGroupWords) + 2 * kWArr;  // the helper's
+    constexpr int kZ = 12;  // a zero slot of A_
+    w_put(A_, w.l, fq_select(w.l >= 12, widen<2>(fq_zero()), a));
+    w_put(X_, w.l, w_xi_loose(a));
+    w_sync();
+    const bool hi = w.e >= 3;
+    const int k = hi ? w.e - 3 : w.e, c = w.c;
+    // U = hi ? x + y : (helper ? xi*x : x);  V = hi ? xi*y + x : y
+    const uint32_t* US = (helper && !hi) ? X_ : A_;
+    const uint32_t* VS = hi ? X_ : A_;
+    const Fq<23> u0 = fq_norm(fq_add(w_get<21>(US, 2 * k), w_get<2>(A_, hi ? 2 * k + 6 : kZ)));
+    const Fq<23> u1 = fq_norm(fq_add(w_get<21>(US, 2 * k + 1), w_get<2>(A_, hi ? 2 * k + 7 : kZ)));
+    const auto vo = fq_add(w_get<21>(VS, 2 * k + 6 + c), w_get<2>(A_, hi ? 2 * k + c : kZ));
+    const auto vp = fq_add(w_get<21>(VS, 2 * k + 7 - c), w_get<2>(A_, hi ? 2 * k + 1 - c : kZ));
+    const auto vx = fq_pick(c != 0, vp, fq_neg_lazy(vp));
+    const auto p = fq_dot2(u0, vo, u1, vx);
+    static_assert(kl(decltype(fq_dot2(u0, vo, u1, vx))::kK) == 1 && kv(decltype(fq_dot2(u0, vo, u1, vx))::kK) <= 8,
+                  "w12_cyc32: the products are stored as normalized values <= 8p");
+    w_put(P_, w.l, widen<8>(p));
+    w_sync();
+    // even e: 3*(P_(k+3) - P_k - xi*P_k) - 2*a with k = e/2; odd e: z1 = w^3: 6*P_0 + 2a;
+    // z5 = w^5: 6*P_1 + 2a;  z2 = w^1: 6*xi*P_2 + 2a  (w12_cyc)
+    const int ka = w.e >> 1;
+    const Fq<8> pu = w_get<8>(PM, 2 * (ka + 3) + c), pv = w_get<8>(PM, 2 * ka + c);
+    const Fq<8> pw = w_get<8>(PH, 2 * ka + c);
+    const Fq<8> px = w_get<8>(w.e == 1 ? PH : PM, w.e == 1 ? 4 + c : (w.e >= 3 ? w.e - 3 : 0) + c);
+    const bool even = (w.e & 1) == 0;
+    const auto ta = fq_norm(fq_sub(fq_sub(pu, pv), pw));
+    const auto t = fq_pick(even, ta, fq_dbl(px));
+    const auto a2 = fq_dbl(a);
+    const auto s = fq_pick(even, fq_neg_lazy(a2), a2);
+    return fq_fold(fq_add(fq_add(t, fq_add(t, t)), s));
+}
+// the squaring on the final exponentiation's squarer chain (w12_exp_sq,
+// w12_fe_last_s): kernels_tail.hip runs it on a pair of groups
+#ifndef BN_S_CYC
+#define BN_S_CYC w12_cyc
+#endif
+
 // unitary inverse (fq12.rs:126-128): the w^odd coefficients negate
 __device__ __forceinline__ Fq<2> w12_conj(const Fq<2>& a) {
     const WL w = wl();
@@ -550,7 +609,7 @@ __device__ __noinline__ Fq<2> w12_exp_sq(Fq<2> x, WDuo& d) {
     for (int k = 0;; ++k) {
         if ((kZNaf.nz >> k) & 1u) d.put(x);
         if (k == kZNaf.top) break;
-        x = w12_cyc(x);
+        x = BN_S_CYC(x);
     }
     return d.get_result();
 }
@@ -574,12 +633,12 @@ __device__ __noinline__ Fq<2> w12_exp_mul(WDuo& d) {
 // forms m, n and q (the reference's names, fq12.rs:75-105).
 __device__ __noinline__ Fq<2> w12_fe_last_s(Fq<2> s, WDuo& d) {
     const Fq<2> a = w12_exp_sq(s, d);
-    const Fq<2> b = w12_cyc(a);
+    const Fq<2> b = BN_S_CYC(a);
     d.put(b);
-    const Fq<2> c = w12_cyc(b);
+    const Fq<2> c = BN_S_CYC(b);
     const Fq<2> dd = w12_mul(c, b);
     const Fq<2> e = w12_exp_sq(dd, d);
-    const Fq<2> f1 = w12_cyc(e);
+    const Fq<2> f1 = BN_S_CYC(e);
     const Fq<2> g = w12_exp_sq(f1, d);
     const Fq<2> j = w12_mul(w12_conj(g), e);
     const Fq<2> k = w12_mul(j, w12_conj(dd));

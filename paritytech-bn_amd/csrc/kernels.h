@@ -568,6 +568,11 @@ __global__ void __launch_bounds__(kBlock) k_fe_wide(const uint32_t* __restrict__
 __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __restrict__ in, size_t in_stride,
                                                              SetSpan sets, uint32_t* __restrict__ out,
                                                              size_t out_stride, size_t out_base, size_t out_set, int per_group);
+// kernels_tail.hip: k_horner_tree's recombination + final exponentiation of ONE
+// product, the final exponentiation's squarer on a pair of 16-lane groups (w12_cyc32)
+constexpr int kTailBlock = 256;
+__global__ void __launch_bounds__(kTailBlock) k_horner_tree2(const uint32_t* __restrict__ g, SegPlan plan, int do_fe,
+                                                             bn_gt* __restrict__ out, int* __restrict__ err);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
 // (a producer wave for the lines, consumer groups for the wide Miller loop + FE)
 constexpr int kLatPairs = 8;

@@ -25,7 +25,7 @@ os.environ.setdefault("BN254MI_LIB", os.path.join(ROOT, "paritytech-bn_amd", "li
 
 from substrate_bn import _native, synth  # noqa: E402
 
-TUS = ["pairing", "fe", "wide", "latency_w2", "group", "gtpow", "codec", "util", "reduce"]  # every unit (Makefile dbg)
+TUS = ["pairing", "fe", "wide", "latency_w2", "group", "gtpow", "codec", "util", "reduce", "tail"]  # every unit (Makefile dbg)
 
 
 def counters(L):
