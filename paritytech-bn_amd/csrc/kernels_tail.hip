@@ -1,20 +1,26 @@
 // kernels_tail.hip -- k_horner_tree2: the recombination and final exponentiation
 // of ONE product (pairing_batch / miller_loop_batch, mod.rs:609-640, 904-926;
-// fq12.rs:62-110), the tail of config 5: k_horner_tree (kernels_wide.hip) with the
-// final exponentiation's squarer S on a PAIR of 16-lane groups of one wave, which
-// run its cyclotomic squarings with w12_cyc32 (fq12_wide.h: the helper computes
-// the xi * P products beside the main group's P, ~12 % fewer instructions on the
-// chain).  Channel ch < 4: S = groups 2ch, 2ch + 1 (waves 0-1), M = group 8 + ch
-// (wave 2); wave 3 is done after the tree, so every SIMD keeps one wave.  (The
-// first form, 512 threads with every segment on a group pair, put two waves on
-// each SIMD and ran the tail ~0.12 ms slower, profiles/r5h_ab_tail.txt.)  Values
-// are k_horner_tree's.
+// fq12.rs:62-110), the tail of config 5: k_horner_tree (kernels_wide.hip)'s
+// recombination on the 16-lane groups, then the final exponentiation's last chunk
+// on the whole block in the digit-sliced layout (BN_TAIL_DS, fq12_ds.h: one digit
+// per lane, ~1.7x shorter squarings and ~1.5x shorter products than the 16-lane
+// ones on the chain, tools/ds_check).  BN_TAIL_DS=0 builds the round-5 form: the
+// squarer S on a PAIR of 16-lane groups of one wave (w12_cyc32: the helper
+// computes the xi * P products beside the main group's P), channel ch < 4: S =
+// groups 2ch, 2ch + 1 (waves 0-1), M = group 8 + ch (wave 2).  Values are
+// k_horner_tree's.
+#ifndef BN_TAIL_DS
+#define BN_TAIL_DS 1
+#endif
 #define BN_FOLD_LDS 1
 #define BN_WIDE_ARRS 4
 #define BN_S_CYC w12_cyc32
 #include "fq.h"
 #define BN_SPLIT 1
 #include "fq12_wide.h"
+#if BN_TAIL_DS
+#include "fq12_ds.h"
+#endif
 
 namespace bn {
 
@@ -22,7 +28,11 @@ constexpr int kTailThreads = BN_WIDE_THREADS;
 static_assert(kTailThreads == kTailBlock, "the launch (kernels.h kTailBlock) and the LDS layout agree");
 static_assert(kWGroups == 16, "four waves of four groups");
 constexpr int kTailDuo = 4;  // final-exponentiation channels: S pairs in waves 0-1, M in wave 2
+#if BN_TAIL_DS
+static_assert(kDsThreads == kTailThreads, "the digit-sliced element takes the whole block");
+#else
 __shared__ uint32_t g_tail_ch[kTailDuo * kDuoWords];
+#endif
 __shared__ uint32_t g_tail_cnt[kTailDuo * 4];
 __shared__ uint32_t g_tail_zero;
 
@@ -84,6 +94,18 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
     x = w_get<2>(slot(0), w.l);
     __syncthreads();  // slot 0 is group 0's operand area again from here on
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#if BN_TAIL_DS
+    if (do_fe) {
+        const bool zero = g_tail_zero != 0;
+        if (zero && err && threadIdx.x == 0) err_or(err, BN_ERR_FE_ZERO);
+        ds_init();
+        const Fq<2> r = ds_to_w12(ds_fe_last(ds_from_w12(x)));  // every thread; threads 0..11 get the value
+        if (!zero && threadIdx.x < 12) fq_store_ref(r, words);
+    } else {
+        fq_store_ref(x, words);
+    }
+    if (threadIdx.x < 12) st_words(&out[0].c[w_gt_index(w)], words);
+#else
     if (do_fe) {
         if (grp >= 3 * kTailDuo) return;  // wave 3
         const bool m = grp >= 2 * kTailDuo;
@@ -101,6 +123,7 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
         fq_store_ref(x, words);
     }
     if (w.l < 12 && grp == 0) st_words(&out[0].c[w_gt_index(w)], words);
+#endif
 }
 
 }  // namespace bn
