@@ -577,11 +577,31 @@ uint32_t* parts_region(bn_ctx* c, size_t nchunks) {
 // into *d_out: k_horner_tree (the squarings of the segments side by side and a
 // product tree); BN254MI_HORNER_TREE=0 selects k_horner_wide (one group, Horner's
 // rule), kept for A/B
+// Build parameters (A/B builds, tools/build_variant.sh): BN_TAIL_DS=0 builds the tail
+// without the digit-sliced layout (kernels_tail.hip), BN_SEG_FE1=0 keeps the segments'
+// first chunks and squarings inside k_horner_tree2
+#ifndef BN_TAIL_DS
+#define BN_TAIL_DS 1
+#endif
+#ifndef BN_SEG_FE1
+#define BN_SEG_FE1 1
+#endif
 static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out, hipStream_t s) {
     const char* env = getenv("BN254MI_HORNER_TREE");
     const int tree = env ? atoi(env) : 2;  // 2: k_horner_tree2 (default), 1: k_horner_tree, 0: k_horner_wide
-    if (tree == 2 && BN_FE_DUO && plan.S <= kMaxSeg)
-        k_horner_tree2<<<1, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err);
+    if (tree == 2 && BN_FE_DUO && plan.S <= kMaxSeg) {
+        // several segments (config 5): their first chunks and squarings one block each
+        // (k_seg_fe1), the zero flags at the start of the reduction's ping-pong region A
+        // (free once the reduction has written the result region)
+        const uint32_t* zf = nullptr;
+        if (BN_TAIL_DS && BN_SEG_FE1 && do_fe && plan.S > 1) {
+            uint32_t* z = slot_region(c, kRegionA);
+            k_seg_fe1<<<plan.S, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, z);
+            HIPCHK(c, hipGetLastError());
+            zf = z;
+        }
+        k_horner_tree2<<<1, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err, zf);
+    }
     else if (tree != 0)
         k_horner_tree<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err,
                                            wide_duo(1) ? 1 : 0);

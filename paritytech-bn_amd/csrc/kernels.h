@@ -572,7 +572,13 @@ __global__ void __launch_bounds__(kBlock) k_fq12_reduce_wide(const uint32_t* __r
 // product, the final exponentiation's squarer on a pair of 16-lane groups (w12_cyc32)
 constexpr int kTailBlock = 256;
 __global__ void __launch_bounds__(kTailBlock) k_horner_tree2(const uint32_t* __restrict__ g, SegPlan plan, int do_fe,
-                                                             bn_gt* __restrict__ out, int* __restrict__ err);
+                                                             bn_gt* __restrict__ out, int* __restrict__ err,
+                                                             const uint32_t* __restrict__ zf);
+// pairing_batch with several segments: one block per segment runs the first chunk of
+// the final exponentiation and the segment's Horner squarings (digit-sliced, fq12_ds.h)
+// in place, zf[s] = segment s's value is zero; then k_horner_tree2 with zf
+__global__ void __launch_bounds__(kTailBlock) k_seg_fe1(uint32_t* __restrict__ g, SegPlan plan,
+                                                        uint32_t* __restrict__ zf);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
 // (a producer wave for the lines, consumer groups for the wide Miller loop + FE)
 constexpr int kLatPairs = 8;

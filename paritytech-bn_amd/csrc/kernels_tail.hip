@@ -36,14 +36,48 @@ __shared__ uint32_t g_tail_ch[kTailDuo * kDuoWords];
 __shared__ uint32_t g_tail_cnt[kTailDuo * 4];
 __shared__ uint32_t g_tail_zero;
 
+#if BN_TAIL_DS
+// pairing_batch with several segments: block s takes segment s's value g_s (element
+// s of the split-layout array g, stride S), runs the final exponentiation's first
+// chunk on it (w12_fe_first, fq12.rs:62-73: a power map, so E1(prod g_s^(2^e_s)) =
+// prod E1(g_s)^(2^e_s)) and then its e_s = len_(s+1) + ... + len_(S-1)
+// squarings in the cyclotomic subgroup on the whole block (ds_cyc), and writes the
+// result back in place; zf[s] = 1 when g_s is zero (the product is zero: the
+// reference's final_exponentiation returns None, fq12.rs:63-72).  The segments'
+// squarings run side by side on S CUs instead of on the 16-lane groups of one block.
+__global__ void __launch_bounds__(kTailThreads) k_seg_fe1(uint32_t* __restrict__ g, SegPlan plan,
+                                                          uint32_t* __restrict__ zf) {
+    fold_table_init();
+    const WL w = wl();
+    const int s = (int)blockIdx.x;
+    int e = 0;
+    for (int t = s + 1; t < plan.S; ++t) e += plan.hi[t] - plan.lo[t];
+    Fq<2> x = widen<2>(fq_zero());
+    if (threadIdx.x < (unsigned)kWLanes) {  // group 0
+        x = w_ld_split(g, (size_t)plan.S, (size_t)s, w);
+        const bool zero = w12_is_zero(x);
+        if (threadIdx.x == 0) zf[s] = zero ? 1u : 0u;
+        x = w12_fe_first(x);
+    }
+    ds_init();
+    uint32_t d = ds_from_w12(x);
+#pragma unroll 1
+    for (int k = 0; k < e; ++k) d = ds_cyc(d);
+    x = ds_to_w12(d);
+    if (threadIdx.x < 12) w_st_split(g, (size_t)plan.S, (size_t)s, w, x);
+}
+#endif
+
 // g: the S segment values (element s of a split-layout array of stride S);
 // segment s's value is raised to 2^(len_(s+1) + ... + len_(S-1)), the values are
 // multiplied in a tree, then the final exponentiation's last chunk (do_fe:
 // pairing_batch, after the first chunk on every segment) or the value itself
-// (miller_loop_batch) goes to out[0]
+// (miller_loop_batch) goes to out[0].  zf (do_fe only): k_seg_fe1 has run the
+// first chunk and the squarings already, zf[s] its zero flags.
 __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* __restrict__ g, SegPlan plan,
                                                                int do_fe, bn_gt* __restrict__ out,
-                                                               int* __restrict__ err) {
+                                                               int* __restrict__ err,
+                                                               const uint32_t* __restrict__ zf) {
     if (threadIdx.x == 0) g_tail_zero = 0;
     if (threadIdx.x < kTailDuo * 4) g_tail_cnt[threadIdx.x] = 0;
     __syncthreads();  // the resets are seen before any group can use them
@@ -58,7 +92,10 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
         e0 += plan.hi[t] - plan.lo[t];
         if (t > grp) e += plan.hi[t] - plan.lo[t];
     }
-    if (do_fe) {
+    if (do_fe && zf) {
+        if (threadIdx.x < (unsigned)plan.S && zf[threadIdx.x]) g_tail_zero = 1;
+        e0 = 0;  // k_seg_fe1 did the first chunk and the squarings
+    } else if (do_fe) {
         if (seg && w12_is_zero(x) && w.l == 0) g_tail_zero = 1;
         x = w12_fe_first(x);  // first chunk; of one (groups past S): one
 #pragma unroll 1
