@@ -586,6 +586,10 @@ uint32_t* parts_region(bn_ctx* c, size_t nchunks) {
 #ifndef BN_SEG_FE1
 #define BN_SEG_FE1 1
 #endif
+// BN_TAIL_M=0: the final exponentiation after k_seg_fe1 on one block (no multiplier block)
+#ifndef BN_TAIL_M
+#define BN_TAIL_M 1
+#endif
 static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out, hipStream_t s) {
     const char* env = getenv("BN254MI_HORNER_TREE");
     const int tree = env ? atoi(env) : 2;  // 2: k_horner_tree2 (default), 1: k_horner_tree, 0: k_horner_wide
@@ -594,13 +598,14 @@ static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out
         // (k_seg_fe1), the zero flags at the start of the reduction's ping-pong region A
         // (free once the reduction has written the result region)
         const uint32_t* zf = nullptr;
-        if (BN_TAIL_DS && BN_SEG_FE1 && do_fe && plan.S > 1) {
+        if (BN_TAIL_DS && BN_SEG_FE1 && do_fe && plan.S > 1 && (size_t)kSlotWords * c->cap >= (size_t)kTailChanWords) {
             uint32_t* z = slot_region(c, kRegionA);
             k_seg_fe1<<<plan.S, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, z);
             HIPCHK(c, hipGetLastError());
             zf = z;
         }
-        k_horner_tree2<<<1, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err, zf);
+        k_horner_tree2<<<zf && BN_TAIL_M ? 2 : 1, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err,
+                                                          zf);
     }
     else if (tree != 0)
         k_horner_tree<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err,

@@ -522,4 +522,118 @@ __device__ __noinline__ uint32_t ds_fe_last(uint32_t s) {
     return ds_mul(u, r, false);
 }
 
+// ---------------------------------------------------------------- squarer and multiplier blocks
+// The same last chunk on TWO blocks of one launch (k_horner_tree2 after k_seg_fe1):
+// the squarer block S runs the chain of squarings and hands x^(2^k) at each nonzero
+// NAF digit of u to the multiplier block M through global memory; M multiplies
+// them into its accumulator and hands the result back (fq12_wide.h's two-group
+// final exponentiation, here between CUs of different XCDs).  Every item has its
+// own slot (kDsItems of them, no reuse within a call) and every word carries its
+// stamp: each digit lane stores (1 << 32 | digit) as one agent-scope 64-bit atomic
+// (coherent across the XCDs' L2s) and goes on -- the producer never waits for its
+// stores -- and the consumer's lanes poll their own words until the stamp is there.
+// k_seg_fe1 zeroes the channel before each tail.  A poll that runs out of its cap
+// sets BN_ERR_INTERNAL (the call fails, as fq12_wide.h duo_wait).  (Counters with
+// release / acquire cost the producer ~1.5 us per hand-off, tools/xblock_probe.)
+constexpr int kDsItems = 80;    // S -> M: 3 x 24 powers + b + k
+constexpr int kDsResults = 8;   // M -> S: a, e, g, o, u
+constexpr int kDsChanWords = 2 * 128 * (kDsItems + kDsResults);  // 32-bit words
+struct DsChan {
+    uint64_t* w;  // (kDsItems + kDsResults) x 128 stamped words of global memory
+    int* err;
+    uint32_t items, results;
+};
+__device__ __forceinline__ void ds_chan_st(uint64_t* slot, uint32_t a) {
+    const DsLane x = ds_lane();
+    typedef __attribute__((address_space(1))) uint64_t g64;  // global: global_ (not flat) instructions
+    if (x.dl)
+        __hip_atomic_store((g64*)(slot + 10 * x.cid + x.k), (1ull << 32) | a, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ds_chan_ld(const uint64_t* slot, int* err) {
+    const DsLane x = ds_lane();
+    if (!x.dl) return 0u;
+    typedef const __attribute__((address_space(1))) uint64_t g64;
+    g64* p = (g64*)(slot + 10 * x.cid + x.k);
+    uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t spins = 0; (v >> 32) == 0 && spins < kSpinCap; ++spins) {
+        __builtin_amdgcn_s_sleep(1);
+        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if ((v >> 32) == 0 && err) err_or(err, BN_ERR_INTERNAL);
+    return (uint32_t)v;
+}
+__device__ __forceinline__ void ds_put(DsChan& ch, uint32_t a) {  // S
+    ds_chan_st(ch.w + 128 * (ch.items++), a);
+}
+__device__ __forceinline__ uint32_t ds_take(DsChan& ch) {  // M
+    return ds_chan_ld(ch.w + 128 * (ch.items++), ch.err);
+}
+__device__ __forceinline__ void ds_put_result(DsChan& ch, uint32_t a) {  // M
+    ds_chan_st(ch.w + 128 * (kDsItems + ch.results++), a);
+}
+__device__ __forceinline__ uint32_t ds_get_result(DsChan& ch) {  // S
+    return ds_chan_ld(ch.w + 128 * (kDsItems + ch.results++), ch.err);
+}
+// S's side of exp_by_neg_z: x^(2^k) handed over at each nonzero NAF digit of u
+__device__ __noinline__ uint32_t ds_exp_sq(uint32_t xx, DsChan& ch) {
+#pragma unroll 1
+    for (int k = 0;; ++k) {
+        if ((kZNaf.nz >> k) & 1u) ds_put(ch, xx);
+        if (k == kZNaf.top) break;
+        xx = ds_cyc(xx);
+    }
+    return ds_get_result(ch);
+}
+// M's side: the product of the handed-over powers (x^-1 = conj(x) in the cyclotomic
+// subgroup); returns the first item (x itself)
+__device__ __noinline__ uint32_t ds_exp_mul(DsChan& ch) {
+    const uint32_t x0 = ds_take(ch);
+    uint32_t acc = (kZNaf.minus & 1u) ? ds_conj(x0) : x0;
+#pragma unroll 1
+    for (int k = 1; k <= kZNaf.top; ++k) {
+        if (!((kZNaf.nz >> k) & 1u)) continue;
+        const uint32_t y = ds_take(ch);
+        acc = ds_mul(acc, y, ((kZNaf.minus >> k) & 1u) != 0);
+    }
+    ds_put_result(ch, ds_conj(acc));
+    return x0;
+}
+// the last chunk (fq12.rs:75-105) of s on S, with M (ds_fe_last_m) beside it: the
+// hand-overs are [24 powers of s], b, [24 powers of d], [24 powers of f1], k; M
+// returns a, e, g, then o = frob(k b) and u = frob^3(conj(s) k b) (fq12_wide.h
+// w12_fe_last_s / w12_final_exp_m, the reference's names)
+__device__ __noinline__ uint32_t ds_fe_last_s(uint32_t s, DsChan& ch) {
+    const uint32_t a = ds_exp_sq(s, ch);
+    const uint32_t b = ds_cyc(a);
+    ds_put(ch, b);
+    const uint32_t c = ds_cyc(b);
+    const uint32_t d = ds_mul(c, b, false);
+    const uint32_t e = ds_exp_sq(d, ch);
+    const uint32_t f1 = ds_cyc(e);
+    const uint32_t g = ds_exp_sq(f1, ch);
+    const uint32_t j = ds_mul(e, g, true);  // conj(g) * e
+    const uint32_t k = ds_mul(j, d, true);  // j * conj(d)
+    ds_put(ch, k);
+    const uint32_t m = ds_mul(k, e, false);
+    const uint32_t n = ds_mul(s, m, false);
+    const uint32_t q = ds_frob<2>(k);
+    const uint32_t o = ds_get_result(ch);
+    const uint32_t p = ds_mul(o, n, false);
+    const uint32_t r = ds_mul(q, p, false);
+    const uint32_t u = ds_get_result(ch);
+    return ds_mul(u, r, false);
+}
+__device__ __noinline__ void ds_fe_last_m(DsChan& ch) {
+    const uint32_t s = ds_exp_mul(ch);  // a
+    const uint32_t b = ds_take(ch);
+    (void)ds_exp_mul(ch);               // e
+    (void)ds_exp_mul(ch);               // g
+    const uint32_t k = ds_take(ch);
+    const uint32_t l = ds_mul(k, b, false);
+    ds_put_result(ch, ds_frob<1>(l));   // o
+    const uint32_t t = ds_mul(l, s, true);  // conj(s) * l
+    ds_put_result(ch, ds_frob<3>(t));   // u
+}
+
 }  // namespace bn

@@ -574,9 +574,13 @@ constexpr int kTailBlock = 256;
 __global__ void __launch_bounds__(kTailBlock) k_horner_tree2(const uint32_t* __restrict__ g, SegPlan plan, int do_fe,
                                                              bn_gt* __restrict__ out, int* __restrict__ err,
                                                              const uint32_t* __restrict__ zf);
+// words of the workspace region behind zf: the zero flags and the channel between
+// k_horner_tree2's squarer and multiplier blocks (fq12_ds.h DsChan)
+constexpr int kTailChanWords = 1024 + 2 * 128 * 88;
 // pairing_batch with several segments: one block per segment runs the first chunk of
 // the final exponentiation and the segment's Horner squarings (digit-sliced, fq12_ds.h)
-// in place, zf[s] = segment s's value is zero; then k_horner_tree2 with zf
+// in place, zf[s] = segment s's value is zero; then k_horner_tree2 with zf on two
+// blocks (the final exponentiation's squarer and multiplier)
 __global__ void __launch_bounds__(kTailBlock) k_seg_fe1(uint32_t* __restrict__ g, SegPlan plan,
                                                         uint32_t* __restrict__ zf);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch

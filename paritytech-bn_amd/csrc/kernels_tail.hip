@@ -45,11 +45,18 @@ __shared__ uint32_t g_tail_zero;
 // result back in place; zf[s] = 1 when g_s is zero (the product is zero: the
 // reference's final_exponentiation returns None, fq12.rs:63-72).  The segments'
 // squarings run side by side on S CUs instead of on the 16-lane groups of one block.
+constexpr int kDsChanOff = 1024;  // the S <-> M channel (8-byte aligned), after the zero flags (kernels.h kTailChanWords)
+static_assert(kDsChanOff + kDsChanWords <= kTailChanWords, "tail channel size");
 __global__ void __launch_bounds__(kTailThreads) k_seg_fe1(uint32_t* __restrict__ g, SegPlan plan,
                                                           uint32_t* __restrict__ zf) {
     fold_table_init();
     const WL w = wl();
     const int s = (int)blockIdx.x;
+    {  // k_horner_tree2's channel: every stamp cleared (the blocks share the words)
+        uint64_t* ch = (uint64_t*)(zf + kDsChanOff);
+        for (int i = s * kTailThreads + (int)threadIdx.x; i < kDsChanWords / 2; i += plan.S * kTailThreads)
+            __hip_atomic_store(ch + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     int e = 0;
     for (int t = s + 1; t < plan.S; ++t) e += plan.hi[t] - plan.lo[t];
     Fq<2> x = widen<2>(fq_zero());
@@ -92,6 +99,14 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
         e0 += plan.hi[t] - plan.lo[t];
         if (t > grp) e += plan.hi[t] - plan.lo[t];
     }
+#if BN_TAIL_DS
+    if (do_fe && zf && blockIdx.x == 1) {  // the multiplier block of the final exponentiation
+        ds_init();
+        DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0};
+        ds_fe_last_m(ch);
+        return;
+    }
+#endif
     if (do_fe && zf) {
         if (threadIdx.x < (unsigned)plan.S && zf[threadIdx.x]) g_tail_zero = 1;
         e0 = 0;  // k_seg_fe1 did the first chunk and the squarings
@@ -136,7 +151,14 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
         const bool zero = g_tail_zero != 0;
         if (zero && err && threadIdx.x == 0) err_or(err, BN_ERR_FE_ZERO);
         ds_init();
-        const Fq<2> r = ds_to_w12(ds_fe_last(ds_from_w12(x)));  // every thread; threads 0..11 get the value
+        uint32_t d = ds_from_w12(x);
+        if (zf && gridDim.x == 2) {  // with the multiplier block (block 1)
+            DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0};
+            d = ds_fe_last_s(d, ch);
+        } else {
+            d = ds_fe_last(d);
+        }
+        const Fq<2> r = ds_to_w12(d);  // every thread; threads 0..11 get the value
         if (!zero && threadIdx.x < 12) fq_store_ref(r, words);
     } else {
         fq_store_ref(x, words);
