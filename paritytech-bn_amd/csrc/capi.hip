@@ -594,11 +594,12 @@ static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out
     const char* env = getenv("BN254MI_HORNER_TREE");
     const int tree = env ? atoi(env) : 2;  // 2: k_horner_tree2 (default), 1: k_horner_tree, 0: k_horner_wide
     if (tree == 2 && BN_FE_DUO && plan.S <= kMaxSeg) {
-        // several segments (config 5): their first chunks and squarings one block each
-        // (k_seg_fe1), the zero flags at the start of the reduction's ping-pong region A
-        // (free once the reduction has written the result region)
+        // pairing_batch: the segments' first chunks and squarings one block each
+        // (k_seg_fe1), the zero flags and the squarer <-> multiplier channel of
+        // k_horner_tree2's two blocks at the start of the reduction's ping-pong region
+        // A (free once the reduction has written the result region)
         const uint32_t* zf = nullptr;
-        if (BN_TAIL_DS && BN_SEG_FE1 && do_fe && plan.S > 1 && (size_t)kSlotWords * c->cap >= (size_t)kTailChanWords) {
+        if (BN_TAIL_DS && BN_SEG_FE1 && do_fe && plan.S >= 1 && (size_t)kSlotWords * c->cap >= (size_t)kTailChanWords) {
             uint32_t* z = slot_region(c, kRegionA);
             k_seg_fe1<<<plan.S, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, z);
             HIPCHK(c, hipGetLastError());
