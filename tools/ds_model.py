@@ -1,16 +1,17 @@
 #!/usr/bin/env python3
 """Lane-level model of the digit-sliced Fq12 arithmetic of csrc/fq12_ds.h.
 
-One Fq coordinate per 32-lane slot; 26-bit digits, ten per value, Montgomery
-R = 2^260.  Product columns live at lanes 0..18 (lane j: column j); values
+One Fq coordinate per slot of lanes (the device: 21 lanes, three slots per wave;
+the model: 32, a superset); 26-bit digits, ten per value, Montgomery R = 2^260.
+Product columns live at lanes 0..18 (lane j: column j); values
 (digits) at lanes 10..19 ("digit k at lane 10 + k"), the top digit (lane 19) a
 signed sink that takes every carry out of the lanes below it.  Carries move one
 lane up per DPP wave_shr:1 (shr1 here: lane j gets lane j - 1, lane 0 gets 0).
 The model applies the device's steps lane by lane and checks every bound the
 device code relies on (64-bit columns, 32-bit operands, signed ranges) with
 asserts, and the values against big-integer arithmetic.  Design aid and test of
-the algebra only; the device code is checked against fq12_wide.h on the GPU
-(tests/test_gpu_ds.py).
+the algebra only; the device code is checked against fq12_wide.h on the GPU by
+tools/ds_check.hip (tests/test_gpu_ds.py); tests/test_ds_model.py runs this model.
 
     python tools/ds_model.py [trials]
 """
