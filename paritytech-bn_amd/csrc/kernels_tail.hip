@@ -12,6 +12,11 @@
 #ifndef BN_TAIL_DS
 #define BN_TAIL_DS 1
 #endif
+// k_seg_fe1's first chunk with the Fq12 inversion's products spread over a group's
+// lane pairs (w12_fe_first_par); 0: w12_fe_first on one group (A/B)
+#ifndef BN_FE1_PAR
+#define BN_FE1_PAR 1
+#endif
 #define BN_FOLD_LDS 1
 #define BN_WIDE_ARRS 4
 #define BN_S_CYC w12_cyc32
@@ -35,6 +40,131 @@ __shared__ uint32_t g_tail_ch[kTailDuo * kDuoWords];
 #endif
 __shared__ uint32_t g_tail_cnt[kTailDuo * 4];
 __shared__ uint32_t g_tail_zero;
+
+#if BN_TAIL_DS
+// ---------------------------------------------------------------- the first chunk, in parallel
+// fq12.rs:62-73 of a nonzero f: c = conj(f) * f^-1 = conj(f)^2 * N^-1 with N = f conj(f)
+// = c0^2 - v c1^2 in Fq6 (fq12.rs:305-313: f^-1 = conj(f) N^-1), then frob^2(c) * c.
+// w12_fe_first runs the Fq12 inversion on one lane pair (its ~46 Fq2 products in a
+// row); here the products of each stage of N and of N's inversion (fq6.rs:141-166)
+// are spread over the 8 lane pairs of group 0 (round r: lane pair P takes product
+// P + 8r, operands and results through LDS, one wave: no barrier), while group 4
+// (another wave) squares conj(f).  Inverses are unique, so the value is
+// w12_fe_first's.  Fq2 ids in g_inv (two slots each): 0..5 the coefficients z_e of
+// w^e (c0 = (z0, z2, z4), c1 = (z1, z3, z5)), then the stage results.
+constexpr int kInvIds = 48;
+__shared__ uint32_t g_inv[2 * kInvIds * kWSlot];
+__device__ __forceinline__ Fq2<2> inv_get(int id) {
+    return {w_get<2>(g_inv, 2 * id + (int)(threadIdx.x & 1u))};
+}
+__device__ __forceinline__ void inv_put(int id, const Fq2<2>& v) { w_put(g_inv, 2 * id + (int)(threadIdx.x & 1u), v.c); }
+// one round: lane pair P computes id dst[P] = op1[P] * op2[P] (P < n; a square when op1 == op2)
+struct InvRound {
+    int n;
+    int8_t a[8], b[8], d[8];
+};
+__device__ __forceinline__ void inv_round(const InvRound& r) {
+    const int P = (int)(threadIdx.x >> 1) & 7;
+    const int a = r.a[P < r.n ? P : 0], b = r.b[P < r.n ? P : 0], d = r.d[P < r.n ? P : 0];
+    const Fq2<2> x = inv_get(a), y = inv_get(b);
+    const Fq2<2> z = fq2_fold(fq2_mul(x, y));
+    w_sync();  // every lane pair has read its operands
+    if (P < r.n) inv_put(d, z);
+    w_sync();
+}
+// ids: a0 0, b0 1, a1 2, b1 3, a2 4, b2 5 (z_e = id e)
+enum : int8_t {
+    kA00 = 8, kA11, kA22, kA01, kA02, kA12, kB00, kB11, kB22, kB01, kB02, kB12,  // stage A products
+    kN0 = 20, kN1, kN2,                                                           // N = c0^2 - v c1^2
+    kM00 = 23, kM11, kM22, kM01, kM02, kM12,                                      // stage B products
+    kC0 = 29, kC1, kC2,                                                           // fq6_inv's c0, c1, c2
+    kU0 = 32, kU1, kU2,                                                           // n2 C1, n1 C2, n0 C0
+    kT = 35, kTi,                                                                 // t, t^-1
+    kT0 = 37, kT1, kT2                                                            // N^-1
+};
+__device__ __noinline__ Fq2<2> inv_xi(const Fq2<2>& x) { return fq2_fold(fq2_mul_xi(x)); }
+// group 0 computes N^-1 (ids kT0..kT2) from the element in ids 0..5
+__device__ __noinline__ void inv_fq6_par() {
+    const int P = (int)(threadIdx.x >> 1) & 7;
+    constexpr InvRound A1 = {8, {0, 2, 4, 0, 0, 2, 1, 3}, {0, 2, 4, 2, 4, 4, 1, 3}, {kA00, kA11, kA22, kA01, kA02, kA12, kB00, kB11}};
+    constexpr InvRound A2 = {4, {5, 1, 1, 3}, {5, 3, 5, 5}, {kB22, kB01, kB02, kB12}};
+    inv_round(A1);
+    inv_round(A2);
+    {  // N0 = a0^2 + xi (2 a1a2) - xi (b1^2 + 2 b0b2); N1 = 2 a0a1 + xi a2^2 - b0^2 - xi (2 b1b2);
+       // N2 = a1^2 + 2 a0a2 - 2 b0b1 - xi b2^2  (lane pairs 0, 1, 2; each computes its own)
+        const int i = P < 3 ? P : 0;
+        const Fq2<2> g0 = inv_get(i == 0 ? kA00 : i == 1 ? kA01 : kA11);
+        const Fq2<2> g1 = inv_get(i == 0 ? kA12 : i == 1 ? kA22 : kA02);
+        const Fq2<2> h0 = inv_get(i == 0 ? kB11 : i == 1 ? kB00 : kB01);
+        const Fq2<2> h1 = inv_get(i == 0 ? kB02 : i == 1 ? kB12 : kB22);
+        // N0 = g0 + xi (2 g1 - h0 - 2 h1); N1 = 2 g0 + xi g1 - h0 - xi 2 h1; N2 = g0 + 2 g1 - 2 h0 - xi h1
+        Fq2<2> nv;
+        if (i == 0) {
+            nv = fq2_fold(fq2_add(g0, inv_xi(fq2_fold(fq2_sub(fq2_dbl(g1), fq2_add(h0, fq2_dbl(h1)))))));
+        } else if (i == 1) {
+            nv = fq2_fold(fq2_sub(fq2_add(fq2_dbl(g0), inv_xi(fq2_fold(fq2_sub(g1, fq2_dbl(h1))))), h0));
+        } else {
+            nv = fq2_fold(fq2_sub(fq2_add(g0, fq2_dbl(g1)), fq2_add(fq2_dbl(h0), inv_xi(h1))));
+        }
+        w_sync();
+        if (P < 3) inv_put(kN0 + i, nv);
+        w_sync();
+    }
+    // fq6_inv (fq6.rs:141-166) of N = (n0, n1, n2)
+    constexpr InvRound B = {6, {kN0, kN1, kN2, kN0, kN0, kN1, 0, 0}, {kN0, kN1, kN2, kN1, kN2, kN2, 0, 0},
+                            {kM00, kM11, kM22, kM01, kM02, kM12, 0, 0}};
+    inv_round(B);
+    {  // C0 = n0^2 - xi n1n2, C1 = xi n2^2 - n0n1, C2 = n1^2 - n0n2
+        const int i = P < 3 ? P : 0;
+        const Fq2<2> u = inv_get(i == 0 ? kM00 : i == 1 ? kM22 : kM11);
+        const Fq2<2> v = inv_get(i == 0 ? kM12 : i == 1 ? kM01 : kM02);
+        const Fq2<2> cv = i == 0 ? fq2_fold(fq2_sub(u, inv_xi(v))) : i == 1 ? fq2_fold(fq2_sub(inv_xi(u), v))
+                                                                     : fq2_fold(fq2_sub(u, v));
+        w_sync();
+        if (P < 3) inv_put(kC0 + i, cv);
+        w_sync();
+    }
+    constexpr InvRound Cr = {3, {kN2, kN1, kN0, 0, 0, 0, 0, 0}, {kC1, kC2, kC0, 0, 0, 0, 0, 0}, {kU0, kU1, kU2, 0, 0, 0, 0, 0}};
+    inv_round(Cr);
+    {  // t = n0 C0 + xi (n2 C1 + n1 C2), t^-1 (every lane pair: the same value)
+        const Fq2<2> t = fq2_fold(fq2_add(inv_get(kU2), inv_xi(fq2_fold(fq2_add(inv_get(kU0), inv_get(kU1))))));
+        const Fq2<2> ti = fq2_fold(fq2_inv(t));
+        w_sync();
+        if (P == 0) inv_put(kTi, ti);
+        w_sync();
+    }
+    constexpr InvRound E = {3, {kC0, kC1, kC2, 0, 0, 0, 0, 0}, {kTi, kTi, kTi, 0, 0, 0, 0, 0}, {kT0, kT1, kT2, 0, 0, 0, 0, 0}};
+    inv_round(E);
+}
+// w12_fe_first of f (group 0 holds f; every thread of the block calls, threads < 256);
+// returns the first chunk on group 0
+__device__ __noinline__ Fq<2> w12_fe_first_par(Fq<2> f) {
+    const WL w = wl();
+    const int grp = (int)threadIdx.x / kWLanes;
+    if (grp == 0 && w.l < 12) w_put(g_inv, w.l, f);  // ids 0..5: lane l = 2e + c is slot l
+    __syncthreads();
+    Fq<2> sq = f;
+    if (grp == 0) {
+        inv_fq6_par();
+    } else if (grp == 4) {  // another wave: conj(f)^2 beside the inversion
+        const int l = w.l < 12 ? w.l : 10 + (w.l & 1);
+        sq = w12_square(w12_conj(w_get<2>(g_inv, l)));
+    }
+    __syncthreads();
+    if (grp == 4 && w.l < 12) w_put(g_inv, 2 * 40 + w.l, sq);  // ids 40..45: conj(f)^2
+    __syncthreads();
+    Fq<2> r = f;
+    if (grp == 0) {
+        const Fq<2> s2 = w_get<2>(g_inv, 2 * 40 + (w.l < 12 ? w.l : 10 + (w.l & 1)));
+        // N^-1 as an Fq12 with c1 = 0: coefficient w^(2j) = T_j, odd w-exponents zero
+        const Fq<2> tv = w_get<2>(g_inv, 2 * (kT0 + (w.e >> 1)) + w.c);
+        const Fq<2> t12 = fq_select((w.e & 1) != 0, widen<2>(fq_zero()), tv);
+        const Fq<2> c = w12_mul(s2, t12);  // conj(f) * f^-1
+        r = w12_mul(w12_frob<2>(c), c);
+    }
+    return r;
+}
+#endif
 
 #if BN_TAIL_DS
 // pairing_batch with several segments: block s takes segment s's value g_s (element
@@ -64,8 +194,12 @@ __global__ void __launch_bounds__(kTailThreads) k_seg_fe1(uint32_t* __restrict__
         x = w_ld_split(g, (size_t)plan.S, (size_t)s, w);
         const bool zero = w12_is_zero(x);
         if (threadIdx.x == 0) zf[s] = zero ? 1u : 0u;
-        x = w12_fe_first(x);
     }
+#if BN_FE1_PAR
+    x = w12_fe_first_par(x);  // group 0 gets the first chunk
+#else
+    if (threadIdx.x < (unsigned)kWLanes) x = w12_fe_first(x);
+#endif
     ds_init();
     uint32_t d = ds_from_w12(x);
 #pragma unroll 1
