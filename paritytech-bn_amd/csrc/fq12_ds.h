@@ -315,6 +315,21 @@ __device__ __forceinline__ uint32_t ds_fold(int64_t y, const DsLane& x) {
 }
 
 // ---------------------------------------------------------------- operations
+// Diagnostic (tools/ds_check.hip built with -DBN_DS_STAMPS=1): thread 0 adds the
+// clocks of each phase of ds_cyc to g_ds_stamp[phase]
+#if defined(BN_DS_STAMPS) && BN_DS_STAMPS
+__shared__ unsigned long long g_ds_stamp[8];
+#define DS_STAMP(i)                                                 \
+    do {                                                            \
+        const unsigned long long t_ = clock64();                    \
+        if (threadIdx.x == 0) g_ds_stamp[i] += t_ - ds_t0;           \
+        ds_t0 = t_;                                                 \
+    } while (0)
+#define DS_STAMP_INIT unsigned long long ds_t0 = clock64()
+#else
+#define DS_STAMP(i) ((void)0)
+#define DS_STAMP_INIT ((void)0)
+#endif
 // this lane's column of u * v: u broadcast (ten digits), v's window at w (words j+1..j+10)
 __device__ __forceinline__ uint64_t ds_col(const uint32_t (&u)[10], const uint32_t* w, uint64_t a = 0) {
 #pragma unroll
@@ -326,10 +341,12 @@ __device__ __forceinline__ uint64_t ds_col(const uint32_t (&u)[10], const uint32
 // slot (e, c), e < 3: P_e = x y of pair e = (w^e, w^(e+3)); e >= 3: Q = (x + y)(xi y + x)
 // of pair e - 3; then every output coordinate from them (kDsComb)
 __device__ __noinline__ uint32_t ds_cyc(uint32_t a) {
+    DS_STAMP_INIT;
     const DsLane x = ds_lane();
     const int wk = ds_wk(x);
     g_ds.E[x.cid][wk] = a;
     __syncthreads();
+    DS_STAMP(0);
     const bool hi = x.e >= 3;
     const int kk = hi ? x.e - 3 : x.e;
     {
@@ -346,6 +363,7 @@ __device__ __noinline__ uint32_t ds_cyc(uint32_t a) {
         }
     }
     ds_order();
+    DS_STAMP(1);
     uint32_t u0[10], u1[10];
     ds_ld10(&g_ds.U0[x.cid][0], u0);
     ds_ld10(&g_ds.U1[x.cid][0], u1);
@@ -353,15 +371,21 @@ __device__ __noinline__ uint32_t ds_cyc(uint32_t a) {
     const uint64_t a2 = ds_col(u1, &g_ds.V1[x.cid][x.j + 1]);
     // c0 = u0 v0 - u1 v1, c1 = u0 v1 + u1 v0
     const int64_t T = (int64_t)a1 + (x.c ? (int64_t)a2 : -(int64_t)a2);
+    DS_STAMP(2);
     const int32_t p = ds_redc(T, x);
     g_ds.PR[x.cid][wk] = p;
     const DsComb cb = g_ds.KC[x.cid];
+    DS_STAMP(3);
     __syncthreads();
+    DS_STAMP(4);
     int64_t y = ds_mad_i(cb.e, (int32_t)a, 0);
     y = ds_mad_i(cb.a, g_ds.PR[cb.i1][wk], y);
     y = ds_mad_i(cb.b, g_ds.PR[cb.i2][wk], y);
     y = ds_mad_i(cb.c, g_ds.PR[cb.i3][wk], y);
-    return ds_fold(x.dl ? y : 0, x);
+    DS_STAMP(5);
+    const uint32_t r = ds_fold(x.dl ? y : 0, x);
+    DS_STAMP(6);
+    return r;
 }
 
 // a * b (fq12.rs:319-327) on the w-basis: out_e = sum_i a'_i b_(e - i mod 6) with

@@ -92,6 +92,9 @@ __global__ void __launch_bounds__(kDsThreads) k_ds_time(const uint32_t* __restri
     if (t < 16)
         for (int i = 0; i < 9; ++i) a.v[i] = in[l * 9 + i];
     uint32_t da = ds_from_w12(a);
+#if defined(BN_DS_STAMPS) && BN_DS_STAMPS
+    if (threadIdx.x < 8) g_ds_stamp[threadIdx.x] = 0;
+#endif
     __syncthreads();
     const unsigned long long t0 = clock64();
     if (which == 0) {
@@ -105,6 +108,9 @@ __global__ void __launch_bounds__(kDsThreads) k_ds_time(const uint32_t* __restri
     const unsigned long long t1 = clock64();
     sink[t] = da + a.v[0];
     if (t == 0) *cyc = t1 - t0;
+#if defined(BN_DS_STAMPS) && BN_DS_STAMPS
+    if (which == 0 && t < 8) cyc[1 + t] = g_ds_stamp[t];
+#endif
 }
 
 #define CK(x)                                                                        \
@@ -132,7 +138,7 @@ int main(int argc, char** argv) {
     unsigned long long* d_cyc;
     CK(hipMalloc(&d_in, h.size() * 4));
     CK(hipMalloc(&d_out, (size_t)n * 12 * 18 * 4));
-    CK(hipMalloc(&d_cyc, (size_t)n * 8));
+    CK(hipMalloc(&d_cyc, (size_t)(n < 16 ? 16 : n) * 8));
     CK(hipMalloc(&d_sink, kDsThreads * 4));
     CK(hipMemcpy(d_in, h.data(), h.size() * 4, hipMemcpyHostToDevice));
     std::vector<uint32_t> o((size_t)n * 12 * 18);
@@ -169,6 +175,14 @@ int main(int argc, char** argv) {
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(&c, d_cyc, 8, hipMemcpyDeviceToHost));
         printf("latency %-8s %.0f clocks per op (%d dependent ops)\n", tn[w], (double)c / iters, iters);
+#if defined(BN_DS_STAMPS) && BN_DS_STAMPS
+        if (w == 0) {
+            unsigned long long st[8];
+            CK(hipMemcpy(st, d_cyc + 1, 64, hipMemcpyDeviceToHost));
+            const char* ph[] = {"E write + barrier", "operand build", "product MADs", "REDC", "barrier 2", "combination", "fold"};
+            for (int i = 0; i < 7; ++i) printf("  ds_cyc phase %-18s %6.0f clocks\n", ph[i], (double)st[i] / iters);
+        }
+#endif
     }
     printf(bad_total ? "DS CHECK FAILED\n" : "DS CHECK OK\n");
     return bad_total ? 1 : 0;
