@@ -261,6 +261,29 @@ def test_g1_mul_two_chain_odd_tail(ctx):
     assert np.array_equal(got[rows], O.g1_mul(base[rows], S[rows], NT))
 
 
+@pytest.mark.parametrize("n", [(1 << 16) + 1, (1 << 17) + 3])
+def test_g2_mul_two_chain_odd_tail(ctx, n):
+    """G2 * Fr at odd sizes past 2^16.  In a BN_G2_MUL2=1 build these take the
+    two-chains-per-lane-pair kernels (k_g2_mul2_split_w at 2^16 + 1, k_g2_mul2_split
+    at 2^17 + 3; pair i runs rows i and i + h, h = ceil(n / 2), the last pair has one
+    chain; profiles/r5s_ab_g2_mul2.txt); the default build runs k_g2_mul_split.  Zero
+    bases, zero scalars, k = 1 and k = r - 1 planted in both halves; rows around 0,
+    h and the tail checked against the oracle on the raw Jacobian image."""
+    h = (n + 1) // 2
+    _, S = O.random_scalars(n, seed=555 + n % 7, lo=0)
+    base = ctx.g2_mul_many(np.tile(O.g2_one(), (n, 1)), np.roll(S, 13, axis=0))  # z != 1
+    one = O.canon_to_mont_array([1]).reshape(4)
+    for row in (1, h + 1, n - 1):
+        base[row] = 0
+        base[row, 8:12] = one                         # G2::zero(): y = (1, 0)
+    S[[2, h + 2, n - 2]] = 0
+    S[[3, h + 3]] = O.canon_to_mont_array([1], O.FR).reshape(4)
+    S[[4, h + 4]] = O.canon_to_mont_array([O.R - 1], O.FR).reshape(4)
+    got = ctx.g2_mul_many(base, S)
+    rows = np.r_[0:48, h - 48:h + 48, n - 48:n]
+    assert np.array_equal(got[rows], O.g2_mul(base[rows], S[rows], NT))
+
+
 # ---- the throughput path (the kernels `value` measures) on the edge cases, vs the oracle
 def test_throughput_path_pairing_many(ctx_tp, pairs):
     p, q = pairs
