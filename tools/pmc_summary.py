@@ -61,13 +61,13 @@ if db is not None:
 # ---- PMC passes
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 prod = collections.defaultdict(lambda: collections.defaultdict(list))  # the config-5 product's kernels
-for sub in ("pmc_prod_fetch", "pmc_prod_write"):
+for sub in ("pmc_prod_fetch", "pmc_prod_write", "pmc_prod_sq"):
     db = one_db(sub + "/*results.db")
     if db is None:
         continue
     for kname, cname, val in db.execute("select kernel_name, counter_name, value from counters_collection"):
         prod[short(kname)][cname].append(float(val))
-for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_g1_fetch", "pmc_g1_write", "pmc_g1_sq"):
+for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_g1_fetch", "pmc_g1_write", "pmc_g1_sq", "pmc_g2_sq"):
     db = one_db(sub + "/*results.db")
     if db is None:
         continue
@@ -139,11 +139,13 @@ for k, v in sorted(agg.items()):
                           "WRITE_SIZE as counted (MI355X_MICROARCH §HBM); source %s" % tag}
     lines.append("%-16s %14.3e %14.3e %14.3e %12.3e %10.3f" % (k, fetch, write, valu, cyc, valu / cyc if cyc else 0))
 if prod:
-    # one product step = one k_horner_tree launch; its traffic is every launch's bytes in the pass
-    steps = len(prod.get("k_horner_tree", {}).get("FETCH_SIZE", [])) or 1
+    # one product step = one launch of the last kernel (k_horner_tree2 since round 5, k_horner_tree
+    # before); its traffic is every launch's bytes in the pass
+    steps = (len(prod.get("k_horner_tree2", {}).get("FETCH_SIZE", []))
+             or len(prod.get("k_horner_tree", {}).get("FETCH_SIZE", [])) or 1)
     per_kernel = {}
     product_kernels = ("k_prepare_wide", "k_prepare", "k_miller_seg", "k_fq12_reduce_wide", "k_horner_tree",
-                       "k_horner_wide", "k_pairing_latency", "k_err_status")  # not the bench's input generation
+                       "k_horner_tree2", "k_seg_fe1", "k_horner_wide", "k_pairing_latency", "k_err_status")  # not the bench's input generation
     for k, v in prod.items():
         if k not in product_kernels:
             continue
@@ -151,6 +153,11 @@ if prod:
         w = sum(v.get("WRITE_SIZE", [])) * 1024 / steps
         per_kernel[k] = {"fetch_bytes_raw": f, "write_bytes": w,
                          "hbm_bytes": (f / read_factor if read_factor else f) + w}
+        if v.get("SQ_WAVES"):  # the product SQ pass: VALU instructions and cycles per wave
+            waves = sum(v["SQ_WAVES"]) / len(v["SQ_WAVES"])
+            per_kernel[k]["valu_insts_per_wave"] = sum(v.get("SQ_INSTS_VALU", [0])) / len(v["SQ_WAVES"]) / waves
+            per_kernel[k]["wave_cycles"] = sum(v.get("SQ_WAVE_CYCLES", [0])) * 4 / len(v["SQ_WAVES"]) / waves
+            per_kernel[k]["waves_per_launch"] = waves
     summary["product_step"] = {
         "hbm_bytes_per_step": sum(x["hbm_bytes"] for x in per_kernel.values()), "per_kernel": per_kernel,
         "steps_in_pass": steps, "read_factor": read_factor, "read_factor_source": factor_src,
