@@ -709,6 +709,19 @@ BN_INLINE auto fq12_mul_by_024(const Fq12<F>& f, const Fq2<X>& ell_0, const Fq2<
 }
 
 // fq12.rs:198-247 -- Granger-Scott cyclotomic squaring (the reference's formula)
+// BN_CYC_LAZY: t0, t2, t4 and xi*t5 leave with a carry pass instead of a fold (their
+// digits normalized, the value bound carried on to the outputs' folds): 65 VALU fewer
+// per square with the asm column sums, k_pairing_full 7.47-7.48 -> 7.37-7.38 ms,
+// Gt::pow -1.2 % (profiles/r5u_ab_cyc_lazy.txt).  Every fold stays under the bound
+// check (fq.h fold_fetch; tools/fold_check.py).
+#ifndef BN_CYC_LAZY
+#define BN_CYC_LAZY 1
+#endif
+#if BN_CYC_LAZY
+#define BN_CYC_T(x) fq2_norm(x)
+#else
+#define BN_CYC_T(x) fq2_fold(x)
+#endif
 template <int A>
 BN_INLINE auto fq12_cyclotomic_sqr(const Fq12<A>& a) {
     const auto& z0 = a.c0.c0;
@@ -718,18 +731,18 @@ BN_INLINE auto fq12_cyclotomic_sqr(const Fq12<A>& a) {
     const auto& z1 = a.c1.c1;
     const auto& z5 = a.c1.c2;
     auto tmp01 = fq2_mul(z0, z1);
-    auto t0 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z0, z1), fq2_add(fq2_mul_xi(z1), z0)), tmp01), fq2_mul_xi(tmp01)));
+    auto t0 = BN_CYC_T(fq2_sub(fq2_sub(fq2_mul(fq2_add(z0, z1), fq2_add(fq2_mul_xi(z1), z0)), tmp01), fq2_mul_xi(tmp01)));
     auto t1 = fq2_dbl(tmp01);
     auto tmp23 = fq2_mul(z2, z3);
-    auto t2 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z2, z3), fq2_add(fq2_mul_xi(z3), z2)), tmp23), fq2_mul_xi(tmp23)));
+    auto t2 = BN_CYC_T(fq2_sub(fq2_sub(fq2_mul(fq2_add(z2, z3), fq2_add(fq2_mul_xi(z3), z2)), tmp23), fq2_mul_xi(tmp23)));
     auto t3 = fq2_dbl(tmp23);
     auto tmp45 = fq2_mul(z4, z5);
     auto xi45 = fq2_mul_xi(tmp45);  // also gives xi * t5 = 2 * xi * tmp45 below
-    auto t4 = fq2_fold(fq2_sub(fq2_sub(fq2_mul(fq2_add(z4, z5), fq2_add(fq2_mul_xi(z5), z4)), tmp45), xi45));
+    auto t4 = BN_CYC_T(fq2_sub(fq2_sub(fq2_mul(fq2_add(z4, z5), fq2_add(fq2_mul_xi(z5), z4)), tmp45), xi45));
 
     auto n0 = fq2_add(fq2_dbl(fq2_sub(t0, z0)), t0);
     auto n1 = fq2_add(fq2_dbl(fq2_add(t1, z1)), t1);
-    auto x5 = fq2_fold(fq2_dbl(xi45));  // xi * t5
+    auto x5 = BN_CYC_T(fq2_dbl(xi45));  // xi * t5
     auto n2 = fq2_add(fq2_dbl(fq2_add(x5, z2)), x5);
     auto n3 = fq2_add(fq2_dbl(fq2_sub(t4, z3)), t4);
     auto n4 = fq2_add(fq2_dbl(fq2_sub(t2, z4)), t2);
