@@ -42,6 +42,14 @@ BN_INLINE void g2_precompute(const G2Aff<B>& q, Emit&& emit) {
 }
 
 #if BN_SPLIT
+// BN_DOT6_ASM: each output's six-product column sum as one v_mad_u64_u32 chain
+// (dot2_asm.inc) instead of 17 64-bit column accumulators: k_miller_seg's loop
+// spilled 27 dwords and reloaded 44 per line with the accumulators (scratch 320 ->
+// 72 B per lane), config 5 1.84-1.90 -> 1.76-1.80 ms and its PMC traffic 1.62 ->
+// 0.80 GB per product, k_pairing_full unchanged (profiles/r5w_ab_dot6.txt)
+#ifndef BN_DOT6_ASM
+#define BN_DOT6_ASM 1
+#endif
 // The same product f * (x0 + x4 w^3 + x2 w^4) on the two-lane layout, as six
 // column sums reduced once each.  In the w-basis (f_m = coefficient of w^m:
 // c0.c(m/2) for even m, c1.c((m-1)/2) for odd m; w^6 = xi)
@@ -88,11 +96,24 @@ BN_INLINE Fq12<2> fq12_mul_by_024_lazy(const Fq12<F>& f_in, const Fq2<X>& x0_in,
     // value per lane <= 3 * (2p * 4p + 2p * 5p) = 54 p^2: the reduction is below 1.4 p
     auto out = [&](const Fq<2>& a, const LineOps& va, const Fq<2>& b, const LineOps& vb, const Fq<2>& c,
                    const LineOps& vc) {
+#if BN_DOT6_ASM && BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
+        // the same six-product column sum as one v_mad_u64_u32 chain (dot2_asm.inc
+        // BN_ASM_DOT6): no 17-column accumulator held across the products
+        const Fq<2> pa = fq_partner(a), pb = fq_partner(b), pc = fq_partner(c);
+        Fq<2> r;
+        asm(BN_ASM_DOT6 : BN_ASM_OUT9(r.v)
+            : BN_ASM_IN9(a.v), BN_ASM_IN9(va.y.v), BN_ASM_IN9(pa.v), BN_ASM_IN9(va.w.v), BN_ASM_IN9(b.v),
+              BN_ASM_IN9(vb.y.v), BN_ASM_IN9(pb.v), BN_ASM_IN9(vb.w.v), BN_ASM_IN9(c.v), BN_ASM_IN9(vc.y.v),
+              BN_ASM_IN9(pc.v), BN_ASM_IN9(vc.w.v), BN_ASM_P
+            : BN_ASM_CLOBBER);
+        return Fq2<2>{r};
+#else
         Acc t = {};
         acc_mad2(t, a, va);
         acc_mad2(t, b, vb);
         acc_mad2(t, c, vc);
         return Fq2<2>{acc_redc<2>(t)};
+#endif
     };
     // outputs last-first, each xi*f_k made just before its first use: under the default
     // scheduler 0.7 % faster than first-first with the four xi*f_k up front
