@@ -41,6 +41,11 @@ def main():
     res["pairing_batch"], v = code_of(lambda: ctx.pairing_batch(p, q))
     res["pairing_batch_value_returned"] = v is not None
     res["miller_loop_batch"], _ = code_of(lambda: ctx.miller_loop_batch(q, p))
+    # past the one-launch threshold: the segmented product, whose only capped waits are the
+    # tail's squarer <-> multiplier channel (fq12_ds.h ds_chan_ld, k_horner_tree2 on two blocks)
+    reps = 4224 // n
+    res["pairing_batch_segmented"], v = code_of(lambda: ctx.pairing_batch(np.tile(p, (reps, 1)), np.tile(q, (reps, 1))))
+    res["pairing_batch_segmented_value_returned"] = v is not None
     # the two-group final exponentiation of k_fe_wide (its S <-> M channel waits)
     _, mv = O.miller_loop_batch(q[:1], p[:1])
     f = np.tile(mv.reshape(1, 48), (4, 1))

@@ -2,12 +2,14 @@
 
 The latency kernels hand lines and final-exponentiation items between waves
 through LDS counters whose spin waits are capped (latency_kernel.h,
-fq12_wide.h duo_wait).  A wait that runs out sets BN_ERR_INTERNAL and the call
+fq12_wide.h duo_wait), and the product's digit-sliced tail hands powers between its
+squarer and multiplier blocks through global words whose polls are capped the same
+way (fq12_ds.h ds_chan_ld).  A wait that runs out sets BN_ERR_INTERNAL and the call
 must fail instead of returning a Gt computed from an unpublished slot -- the
 reference panics rather than return a wrong value (src/groups/mod.rs:900).
 
 libbn254mi_cap0.so (`make -C paritytech-bn_amd cap0`, built by
-__graft_entry__.build()) is the product library with those two units built at
+__graft_entry__.build()) is the product library with those units (and the tail) built at
 spin cap 0, so the first wait of each kernel runs out deterministically (the
 consumer's first line needs the producer's to_affine, tens of microseconds).
 The library replaces the product one, so the calls run in a child process
@@ -38,6 +40,9 @@ def test_capped_handoff_fails_the_call():
     assert res["pairing_batch"] == BN_ERR_INTERNAL and not res["pairing_batch_value_returned"], res
     assert res["miller_loop_batch"] == BN_ERR_INTERNAL, res
     assert res["final_exponentiation_many"] == BN_ERR_INTERNAL, res
+    # the segmented product (4,224 terms): the digit-sliced tail's two-block channel
+    assert res["pairing_batch_segmented"] == BN_ERR_INTERNAL, res
+    assert not res["pairing_batch_segmented_value_returned"], res
     # the status-less device call is accepted, and bn_dev_status reports the failure once
     assert res["pairing_many_dev_call"] == BN_OK, res
     assert res["dev_status_after"] == BN_ERR_INTERNAL, res
