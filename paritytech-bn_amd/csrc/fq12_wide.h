@@ -218,6 +218,13 @@ __shared__ uint32_t g_lat_ring[kLatPairs * kLatRing * kLatLineWords];  // 54 KB
 // three nonzero line coefficients b_m of a'_(e-m) * b_m with a'_i = xi * a_i
 // when the index wraps (w^6 = xi): six digit products per lane, one reduction.
 // The same residues as the reference's sparse product.
+// BN_W12_LINE_DOT6: the six digit products of w12_mul_line as one asm chain (as the
+// two-lane line product, pairing.h BN_DOT6_ASM) instead of 17 column accumulators:
+// the two-wave latency kernel at 4,096 pairs 1.58 -> 1.56-1.57 ms, the rest within
+// noise (profiles/r5aa_ab_w12_line_dot6.txt)
+#ifndef BN_W12_LINE_DOT6
+#define BN_W12_LINE_DOT6 1
+#endif
 __device__ __noinline__ Fq<2> w12_mul_line(Fq<2> a, uint32_t ln_off) {
     const WL w = wl();
     const uint32_t* ln = g_lat_ring + ln_off;
@@ -226,8 +233,31 @@ __device__ __noinline__ Fq<2> w12_mul_line(Fq<2> a, uint32_t ln_off) {
     w_put(A_, w.l, a);
     w_put(X_, w.l, w_xi(a));
     w_sync();
-    Acc t = {};
     constexpr int kM[3] = {0, 3, 4};  // w-exponents of x0, x4, x2
+#if BN_W12_LINE_DOT6 && BN_DOT2_ASM && defined(__HIP_DEVICE_COMPILE__)
+    // the six digit products as one v_mad_u64_u32 chain (dot2_asm.inc BN_ASM_DOT6)
+    Fq<2> xs[6];
+    Fq<kLine> ys[6];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int m = kM[q];
+        const bool wrap = m > w.e;
+        const int i = wrap ? w.e - m + 6 : w.e - m;
+        const uint32_t* src = wrap ? X_ : A_;
+        xs[2 * q] = w_get<2>(src, 2 * i);
+        xs[2 * q + 1] = w_get<2>(src, 2 * i + 1);
+        ys[2 * q] = w_get<kLine>(ln, 3 * q + w.c);
+        ys[2 * q + 1] = w_get<kLine>(ln, 3 * q + (w.c ? 0 : 2));
+    }
+    Fq<2> r;
+    asm(BN_ASM_DOT6 : BN_ASM_OUT9(r.v)
+        : BN_ASM_IN9(xs[0].v), BN_ASM_IN9(ys[0].v), BN_ASM_IN9(xs[1].v), BN_ASM_IN9(ys[1].v), BN_ASM_IN9(xs[2].v),
+          BN_ASM_IN9(ys[2].v), BN_ASM_IN9(xs[3].v), BN_ASM_IN9(ys[3].v), BN_ASM_IN9(xs[4].v), BN_ASM_IN9(ys[4].v),
+          BN_ASM_IN9(xs[5].v), BN_ASM_IN9(ys[5].v), BN_ASM_P
+        : BN_ASM_CLOBBER);
+    return r;
+#else
+    Acc t = {};
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
         const int m = kM[q];
@@ -244,6 +274,7 @@ __device__ __noinline__ Fq<2> w12_mul_line(Fq<2> a, uint32_t ln_off) {
     }
     // value <= 6 * 2p * 4p: the reduction is below (48 p / 2^261 + 1) p < 2p
     return acc_redc<2>(t);
+#endif
 }
 // the line x0 + x4 w^3 + x2 w^4 itself as an element (one * line, the first
 // step of the loop from f = one)
