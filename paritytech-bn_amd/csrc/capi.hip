@@ -721,17 +721,10 @@ static void g1_mul_launch(const bn_g1* d_p, const bn_fr* d_k, size_t n, bn_g1* d
 }
 // G2 * Fr on the two-lane layout: 6.97 -> 6.22 ms per 2^16 against the one-lane
 // kernel of rounds 1-3 (profiles/r4m_ab_g2_split.txt)
-#ifndef BN_G2_MUL2
-#define BN_G2_MUL2 0
-#endif
+// (two chains per lane pair, as k_g1_mul2, measured 15 % slower at 2^16: one wave per
+// SIMD; profiles/r5s_ab_g2_mul2.txt, removed after the A/B)
 static void g2_mul_launch(const bn_g2* d_p, const bn_fr* d_k, size_t n, bn_g2* d_out, hipStream_t s) {
-    const size_t lanes2 = kPathLanes * ((n + 1) / 2);  // two chains per lane pair
-    if (BN_G2_MUL2 && lanes2 >= (size_t)256 * kPairBlock)
-        k_g2_mul2_split<<<grid_pair(lanes2), kPairBlock, 0, s>>>(d_p, d_k, n, d_out);
-    else if (BN_G2_MUL2 && lanes2 >= (size_t)256 * kBlock)
-        k_g2_mul2_split_w<<<grid_for(lanes2), kBlock, 0, s>>>(d_p, d_k, n, d_out);
-    else
-        k_g2_mul_split<<<grid_pair(kPathLanes * n), kPairBlock, 0, s>>>(d_p, d_k, n, d_out);
+    k_g2_mul_split<<<grid_pair(kPathLanes * n), kPairBlock, 0, s>>>(d_p, d_k, n, d_out);
 }
 
 template <typename P, typename K>

@@ -611,8 +611,6 @@ __global__ void __launch_bounds__(kBlock) k_gt_store(const uint32_t* __restrict_
 __global__ void __launch_bounds__(kPairBlock) k_g1_mul(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g1* __restrict__ out);
 __global__ void __launch_bounds__(kPairBlock) k_g1_mul2(const bn_g1* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g1* __restrict__ out);
 __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_g2_mul_split(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g2* __restrict__ out);
-__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_g2_mul2_split(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g2* __restrict__ out);
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_g2_mul2_split_w(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n, bn_g2* __restrict__ out);
 // the group law (kernels_group.hip): op codes of k_g1_op / k_g2_op (b may be null for neg / normalize)
 enum GroupOp { kGroupAdd = 0, kGroupSub = 1, kGroupNeg = 2, kGroupNormalize = 3, kGroupEq = 4 };
 __global__ void __launch_bounds__(kBlock) k_g1_op(int op, const bn_g1* a, const bn_g1* b, size_t n, bn_g1* out,

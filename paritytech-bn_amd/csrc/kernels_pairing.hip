@@ -269,92 +269,6 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_g2_mul_split(const 
     st_ref2(out[i].z, r.z);
 }
 
-// Two chains per lane pair (curve.h jac_mul2, as k_g1_mul2): lane pair i multiplies
-// elements i and i + h, h = ceil(n / 2); the odd tail's second chain has the zero
-// scalar.  Each lane keeps its coordinate of the two bases and the two canonical
-// scalars in LDS, word-major ([word][thread]): 2 x (27 + 8) words per thread.
-// kT threads per block: 256 puts one wave on every SIMD at 2^16 multiplications.
-constexpr int kG2Mul2Words = 27;
-constexpr int kG2Mul2Slots = 2 * kG2Mul2Words + 16;
-template <int kT>
-__device__ __forceinline__ void g2_mul2_body(const bn_g2* __restrict__ p, const bn_fr* __restrict__ k, size_t n,
-                                             bn_g2* __restrict__ out) {
-    __shared__ uint32_t lds[kG2Mul2Slots][kT];
-    fold_table_init();
-    const Balance bal = balance_init();
-    const size_t h = (n + 1) / 2;
-    const size_t i = lane_id() / kL;
-    if (i >= h) return;
-    const unsigned tid = threadIdx.x;
-    const size_t j = i + h;
-    const bool has1 = j < n;
-    const size_t j1 = has1 ? j : i;
-    bool z0, z1;
-    int top0, top1;
-    {
-        uint32_t s0[8], s1[8];
-        fr_to_canonical(k[i], s0);
-        fr_to_canonical(k[j1], s1);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) s1[t] = has1 ? s1[t] : 0u;
-        top0 = scalar_top_bit(s0);
-        top1 = scalar_top_bit(s1);
-        const G2J a0 = {widen<kPt>(ld_ref2(p[i].x)), widen<kPt>(ld_ref2(p[i].y)), widen<kPt>(ld_ref2(p[i].z))};
-        const G2J a1 = {widen<kPt>(ld_ref2(p[j1].x)), widen<kPt>(ld_ref2(p[j1].y)), widen<kPt>(ld_ref2(p[j1].z))};
-        z0 = jac_is_zero(a0);
-        z1 = jac_is_zero(a1);
-#pragma unroll
-        for (int w = 0; w < 9; ++w) {
-            lds[w][tid] = a0.x.c.v[w];
-            lds[9 + w][tid] = a0.y.c.v[w];
-            lds[18 + w][tid] = a0.z.c.v[w];
-            lds[kG2Mul2Words + w][tid] = a1.x.c.v[w];
-            lds[kG2Mul2Words + 9 + w][tid] = a1.y.c.v[w];
-            lds[kG2Mul2Words + 18 + w][tid] = a1.z.c.v[w];
-        }
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            lds[2 * kG2Mul2Words + w][tid] = s0[w];
-            lds[2 * kG2Mul2Words + 8 + w][tid] = s1[w];
-        }
-    }
-    // each thread reads only its own column: no barrier needed
-    auto base = [&](int c) {
-        G2J b;
-        const int o = c * kG2Mul2Words;
-#pragma unroll
-        for (int w = 0; w < 9; ++w) {
-            b.x.c.v[w] = lds[o + w][tid];
-            b.y.c.v[w] = lds[o + 9 + w][tid];
-            b.z.c.v[w] = lds[o + 18 + w][tid];
-        }
-        return b;
-    };
-    auto bit = [&](int c, int pos) {
-        return ((lds[2 * kG2Mul2Words + 8 * c + (pos >> 5)][tid] >> (pos & 31)) & 1u) != 0;
-    };
-    G2J r0, r1;
-    jac_mul2<Fq2>(base, bit, z0, z1, top0, top1, r0, r1, [&](int t) { balance_step(bal, (uint32_t)t); });
-    st_ref2(out[i].x, r0.x);
-    st_ref2(out[i].y, r0.y);
-    st_ref2(out[i].z, r0.z);
-    if (has1) {
-        st_ref2(out[j].x, r1.x);
-        st_ref2(out[j].y, r1.y);
-        st_ref2(out[j].z, r1.z);
-    }
-}
-__global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_g2_mul2_split(const bn_g2* __restrict__ p,
-                                                                          const bn_fr* __restrict__ k, size_t n,
-                                                                          bn_g2* __restrict__ out) {
-    g2_mul2_body<kPairBlock>(p, k, n, out);
-}
-__global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_g2_mul2_split_w(const bn_g2* __restrict__ p,
-                                                                        const bn_fr* __restrict__ k, size_t n,
-                                                                        bn_g2* __restrict__ out) {
-    g2_mul2_body<kBlock>(p, k, n, out);
-}
-
 }  // namespace bn
 
 BN_EXPORT_FOLD_CHECK(pairing)

@@ -263,12 +263,10 @@ def test_g1_mul_two_chain_odd_tail(ctx):
 
 @pytest.mark.parametrize("n", [(1 << 16) + 1, (1 << 17) + 3])
 def test_g2_mul_two_chain_odd_tail(ctx, n):
-    """G2 * Fr at odd sizes past 2^16.  In a BN_G2_MUL2=1 build these take the
-    two-chains-per-lane-pair kernels (k_g2_mul2_split_w at 2^16 + 1, k_g2_mul2_split
-    at 2^17 + 3; pair i runs rows i and i + h, h = ceil(n / 2), the last pair has one
-    chain; profiles/r5s_ab_g2_mul2.txt); the default build runs k_g2_mul_split.  Zero
+    """G2 * Fr at odd sizes past 2^16 (k_g2_mul_split; written for the two-chains-per-pair
+    kernels of profiles/r5s_ab_g2_mul2.txt, which ran pair i on rows i and i + h).  Zero
     bases, zero scalars, k = 1 and k = r - 1 planted in both halves; rows around 0,
-    h and the tail checked against the oracle on the raw Jacobian image."""
+    h = ceil(n / 2) and the tail checked against the oracle on the raw Jacobian image."""
     h = (n + 1) // 2
     _, S = O.random_scalars(n, seed=555 + n % 7, lo=0)
     base = ctx.g2_mul_many(np.tile(O.g2_one(), (n, 1)), np.roll(S, 13, axis=0))  # z != 1
