@@ -316,6 +316,12 @@ constexpr int kRegionParts = 3;            // per-chunk partial products
 constexpr int kRegionResult = 4;           // the final product (element 0, stride 1)
 constexpr size_t kWideGroups = kBlock / 16;  // k_fq12_reduce_wide: 16-lane groups per block
 constexpr size_t kReduceBlocksMax = 512;      // one round of 256-thread blocks, two per CU (kernels_reduce.hip)
+// BN_REDUCE_LAST: a level whose sets all fit one block with chains of up to 8 factors
+// finishes there (config 5: 80 + 24 + 19 -> 85 + 30 us, profiles/r5af_ab_reduce_last.txt)
+#ifndef BN_REDUCE_LAST
+#define BN_REDUCE_LAST 1
+#endif
+constexpr int kReduceLastMax = 8;  // the longest chain a finishing level may take
 
 // sets y < `sets` of n elements each at y * n
 static SetSpan uniform_span(int sets, size_t n) {
@@ -356,6 +362,14 @@ int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, SetSpan span, 
         };
         int per_group = 2;
         while (per_group < 64 && blocks_for(per_group) > kReduceBlocksMax) per_group *= 2;
+#if BN_REDUCE_LAST
+        // a level whose every set fits one block with chains of <= kReduceLastMax factors
+        // finishes there instead of leaving a few blocks per set for one more launch
+        size_t nmax = 0;
+        for (int y = 0; y < sets; ++y) nmax = std::max<size_t>(nmax, span.n[y]);
+        if (nmax > kWideGroups * (size_t)per_group && nmax <= kWideGroups * (size_t)kReduceLastMax)
+            while (kWideGroups * (size_t)per_group < nmax) per_group *= 2;
+#endif
         const size_t per_block = kWideGroups * (size_t)per_group;
         size_t bmax = 0;
         span.blk[0] = 0;
