@@ -89,6 +89,18 @@ def device_points(ctx, n, seed_g1, seed_g2, dev, sh):
     return P, Q
 
 
+ORACLE_BUILD = "oracle/Makefile: gcc -O3 -march=x86-64-v3 (not -march=native: on a Zen 5 host this understates the CPU)"
+
+
+def emit(res):
+    """Print the one JSON line; a cpu_baseline names the oracle's build flags."""
+    cb = res.get("cpu_baseline")
+    if isinstance(cb, dict) and cb.get("kind") == "port":
+        cb["build"] = ORACLE_BUILD
+        cb["sample"] = cb.get("sample", "") + "; built " + ORACLE_BUILD.split(": ", 1)[1]
+    print(json.dumps(res), flush=True)
+
+
 def host_cpus():
     """The CPUs this process may use (affinity set, capped by a cgroup CPU quota)
     and the host CPU model.  On the GPU box os.cpu_count() shows the whole
@@ -259,8 +271,11 @@ def other_workload(args, local_rank):
                                              gst.data_ptr(), sh)
         unit = "pairing-product terms/s"
         res["config"] = {"workload": "BASELINE config 5: one pairing_batch over 2^14 terms, HBM-resident inputs "
-                                     "(bn_pairing_batch_dev: per-term lines + Miller values, device product "
-                                     "reduction and one final exponentiation on 16-lane groups)", "terms": n}
+                                     "(bn_pairing_batch_dev: per-term lines (k_prepare_wide), the segmented "
+                                     "shared-squaring Miller loop (k_miller_seg), the device product reduction "
+                                     "(k_fq12_reduce_wide, one or two levels), then per segment the final "
+                                     "exponentiation's first chunk and Horner squarings (k_seg_fe1) and the tree + "
+                                     "last chunk digit-sliced on two blocks (k_horner_tree2))", "terms": n}
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -274,7 +289,7 @@ def other_workload(args, local_rank):
     el = time.perf_counter() - t0
     res.update({"metric": unit, "value": n * args.steps / el, "unit": unit, "ms_per_step": el / args.steps * 1e3})
     if args.no_cpu_baseline:  # profiler passes: the kernels only
-        print(json.dumps(res), flush=True)
+        emit(res)
         return
     from oracle import oracle as O  # the checker (cpu_baseline leg)
     if args.workload == "product":
@@ -289,8 +304,8 @@ def other_workload(args, local_rank):
                            "traffic_source": "profiles/pmc_summary.json product_step: FETCH_SIZE (read-factor "
                                              "corrected) + WRITE_SIZE of every kernel of one product, committed "
                                              "rocprofv3 PMC passes, not measured in this run",
-                           "kernel": "whole product (k_prepare_wide, k_miller_seg, k_fq12_reduce_wide x2, "
-                                     "k_horner_tree)",
+                           "kernel": "whole product (k_prepare_wide, k_miller_seg, k_fq12_reduce_wide, "
+                                     "k_seg_fe1, k_horner_tree2)",
                            "per_step_ms": ms,
                            "basis": "SURVEY.md 8(d) config 5: n*(19+2655+3741) + 2304 + 8767 Fq-mul, x128 MAD32"}
         threads = host_cpus()["usable"]
@@ -361,7 +376,7 @@ def other_workload(args, local_rank):
                                "sample": "%d G1*Fr of the bench inputs (rows 0.. and n/2.., both chains of the "
                                          "first lanes), oracle, %d threads" % (len(rows), threads),
                                "parity_sample_bit_exact": bool(np.array_equal(ref, oh))}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 def codec_workload(args, local_rank):
@@ -453,7 +468,7 @@ def codec_workload(args, local_rank):
     res["cpu_baseline"] = {"value": m / dt, "unit": unit, "cores": threads, "kind": "port",
                            "sample": "%d elements of the bench inputs, oracle, %d threads" % (m, threads),
                            "parity_sample_bit_exact": bool(same)}
-    print(json.dumps(res), flush=True)
+    emit(res)
 
 
 # ============================================================== pairing workload (configs 2 and 4)
@@ -902,7 +917,7 @@ def main():
             log("bench: --form capi is config 4 in one process (no launcher, --workload pairing)")
             return 2
         args.config = 4
-        print(json.dumps(run_capi_multi(args)), flush=True)
+        emit(run_capi_multi(args))
         return 0
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
@@ -935,7 +950,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     res = run_pairing(args, eng, rank, world, dist)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

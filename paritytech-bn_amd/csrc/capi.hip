@@ -427,10 +427,9 @@ constexpr int kRegionSeg = 8;  // k_miller_seg output: plan.total elements from 
 // squaring per digit but the first (36 Fq-mul) and K lines per line of a pair
 // (39 each; two at a nonzero digit, and the last segment's two closing lines).
 static int seg_sq(int d, int e) { return e - d - 1; }
-static int seg_lines(int d, int e) {
-    int L = e == BN_NAF_DIGITS ? 2 : 0;
-    for (int i = d; i < e; ++i) L += 1 + (int)((kNafNonzero >> i) & 1u);
-    return L;
+static int seg_lines(int d, int e) {  // (digits + nonzero digits in [d, e), by popcount)
+    const uint64_t in = (e >= 64 ? ~0ull : (1ull << e) - 1ull) & ~((1ull << d) - 1ull);
+    return (e == BN_NAF_DIGITS ? 2 : 0) + (e - d) + __builtin_popcountll(kNafNonzero & in);
 }
 // (weights from the ISA -- 5,338 VALU per squaring against 4,730 plus the loads per
 // line -- and three settings between them planned no better on the GPU,
@@ -496,7 +495,25 @@ SegPlan seg_plan(size_t n) {
 // keeps it within T, binary-searched on T.  At 2^14 terms: 1,008 against the
 // uniform plan's 1,236 (K = 4 everywhere: 696 to 1,236 per segment).  Each
 // segment's lane pairs are padded to whole 512-thread blocks (256 lane pairs).
+static SegPlan batch_plan_solve(size_t n);
+// The plan depends on n alone: the last few are kept per host thread, so repeated
+// products of one size (config 5) solve it once.
 SegPlan batch_plan(size_t n) {
+    struct Entry {
+        size_t n;
+        SegPlan p;
+    };
+    static thread_local Entry cache[4];
+    static thread_local int used = 0, next = 0;
+    for (int i = 0; i < used; ++i)
+        if (cache[i].n == n) return cache[i].p;
+    const SegPlan p = batch_plan_solve(n);
+    cache[next] = {n, p};
+    next = (next + 1) % 4;
+    if (used < 4) ++used;
+    return p;
+}
+static SegPlan batch_plan_solve(size_t n) {
     int K0 = 1;
     while (K0 < 16 && (size_t)kMaxSeg * ((n + 2 * K0 - 1) / (2 * K0)) >= ((size_t)1 << 16)) K0 *= 2;
     const size_t align = kPairBlock / kPathLanes;
@@ -519,6 +536,7 @@ SegPlan batch_plan(size_t n) {
                     if (kSegWSq * sq + kSegWLine * L > T) break;  // even K = 1 is over T (and grows with e)
                     int K = (T - kSegWSq * sq) / (kSegWLine * L);
                     if (K > 64) K = 64;
+                    if ((size_t)K > n) K = n > 0 ? (int)n : 1;  // no lane pair of dummy one-lines only
                     const size_t v = dp[d][k] + padded(K);
                     if (v < dp[e][k + 1]) {
                         dp[e][k + 1] = v;

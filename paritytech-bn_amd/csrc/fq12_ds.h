@@ -1,4 +1,4 @@
-// fq12_ds.h -- digit-sliced Fq12: ONE element spread over a 384-thread block,
+// fq12_ds.h -- digit-sliced Fq12: ONE element spread over a 256-thread block,
 // one 26-bit digit (or product column) per lane, for the latency-bound chain of
 // a single final exponentiation (pairing_batch's tail, kernels_tail.hip).
 //
@@ -557,47 +557,61 @@ __device__ __noinline__ uint32_t ds_fe_last(uint32_t s) {
 // (coherent across the XCDs' L2s) and goes on -- the producer never waits for its
 // stores -- and the consumer's lanes poll their own words until the stamp is there.
 // k_seg_fe1 zeroes the channel before each tail.  A poll that runs out of its cap
-// sets BN_ERR_INTERNAL (the call fails, as fq12_wide.h duo_wait).  (Counters with
-// release / acquire cost the producer ~1.5 us per hand-off, tools/xblock_probe.)
+// sets BN_ERR_INTERNAL (the call fails, as fq12_wide.h duo_wait) and marks the
+// wave's channel dead: every later take of that wave reads its words once and does
+// not spin again, so a lost stamp or a stalled partner costs one capped wait per
+// wave, not one per item.  (Counters with release / acquire
+// cost the producer ~1.5 us per hand-off, tools/xblock_probe.)
 constexpr int kDsItems = 80;    // S -> M: 3 x 24 powers + b + k
 constexpr int kDsResults = 8;   // M -> S: a, e, g, o, u
 constexpr int kDsChanWords = 2 * 128 * (kDsItems + kDsResults);  // 32-bit words
+// Failure injection for tests/test_gpu_failure.py only (`make chanfail`): the
+// producer's stores are dropped, so every take runs out of its cap.
+#ifndef BN_DS_DROP_STAMPS
+#define BN_DS_DROP_STAMPS 0
+#endif
 struct DsChan {
     uint64_t* w;  // (kDsItems + kDsResults) x 128 stamped words of global memory
     int* err;
     uint32_t items, results;
+    bool dead;  // wave-uniform: a take of this wave has run out of its cap
 };
 __device__ __forceinline__ void ds_chan_st(uint64_t* slot, uint32_t a) {
     const DsLane x = ds_lane();
     typedef __attribute__((address_space(1))) uint64_t g64;  // global: global_ (not flat) instructions
-    if (x.dl)
+    if (x.dl && !BN_DS_DROP_STAMPS)
         __hip_atomic_store((g64*)(slot + 10 * x.cid + x.k), (1ull << 32) | a, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t ds_chan_ld(const uint64_t* slot, int* err) {
+// every lane of the wave takes part (the spin condition is a wave-wide vote, so
+// `dead` stays wave-uniform); digit lanes poll their own word, the others return 0
+__device__ __forceinline__ uint32_t ds_chan_ld(const uint64_t* slot, DsChan& ch) {
     const DsLane x = ds_lane();
-    if (!x.dl) return 0u;
     typedef const __attribute__((address_space(1))) uint64_t g64;
-    g64* p = (g64*)(slot + 10 * x.cid + x.k);
-    uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t spins = 0; (v >> 32) == 0 && spins < kSpinCap; ++spins) {
-        __builtin_amdgcn_s_sleep(1);
-        v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g64* p = (g64*)(slot + 10 * x.cid + (x.dl ? x.k : 0));
+    uint64_t v = x.dl ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (1ull << 32);
+    if (!ch.dead)
+        for (uint32_t spins = 0; __any((v >> 32) == 0) && spins < kSpinCap; ++spins) {
+            __builtin_amdgcn_s_sleep(1);
+            if (x.dl) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    if (__any((v >> 32) == 0)) {  // decided on the words themselves: one that arrived during the last sleep counts
+        if (!ch.dead && ch.err && (threadIdx.x & 63u) == 0) err_or(ch.err, BN_ERR_INTERNAL);
+        ch.dead = true;
     }
-    if ((v >> 32) == 0 && err) err_or(err, BN_ERR_INTERNAL);
-    return (uint32_t)v;
+    return x.dl ? (uint32_t)v : 0u;
 }
 __device__ __forceinline__ void ds_put(DsChan& ch, uint32_t a) {  // S
     ds_chan_st(ch.w + 128 * (ch.items++), a);
 }
 __device__ __forceinline__ uint32_t ds_take(DsChan& ch) {  // M
-    return ds_chan_ld(ch.w + 128 * (ch.items++), ch.err);
+    return ds_chan_ld(ch.w + 128 * (ch.items++), ch);
 }
 __device__ __forceinline__ void ds_put_result(DsChan& ch, uint32_t a) {  // M
     ds_chan_st(ch.w + 128 * (kDsItems + ch.results++), a);
 }
 __device__ __forceinline__ uint32_t ds_get_result(DsChan& ch) {  // S
-    return ds_chan_ld(ch.w + 128 * (kDsItems + ch.results++), ch.err);
+    return ds_chan_ld(ch.w + 128 * (kDsItems + ch.results++), ch);
 }
 // S's side of exp_by_neg_z: x^(2^k) handed over at each nonzero NAF digit of u
 __device__ __noinline__ uint32_t ds_exp_sq(uint32_t xx, DsChan& ch) {

@@ -17,6 +17,9 @@
 #ifndef BN_FE1_PAR
 #define BN_FE1_PAR 1
 #endif
+#ifndef BN_TAIL_LATE_M
+#define BN_TAIL_LATE_M 0
+#endif
 #define BN_FOLD_LDS 1
 #define BN_WIDE_ARRS 4
 #define BN_S_CYC w12_cyc32
@@ -177,15 +180,37 @@ __device__ __noinline__ Fq<2> w12_fe_first_par(Fq<2> f) {
 // squarings run side by side on S CUs instead of on the 16-lane groups of one block.
 constexpr int kDsChanOff = 1024;  // the S <-> M channel (8-byte aligned), after the zero flags (kernels.h kTailChanWords)
 static_assert(kDsChanOff + kDsChanWords <= kTailChanWords, "tail channel size");
+// k_horner_tree2's role word (after the S <= kMaxSeg zero flags): its two blocks hand
+// values over by polling global memory, which needs both resident at once -- HIP
+// does not promise that (another stream's kernels may hold every CU when block 1
+// would start).  So the roles are claimed, not assumed: the multiplier block swaps
+// 0 -> kRoleM when it starts, the squarer block swaps 0 -> kRoleSolo when it reaches
+// the final exponentiation.  Whichever comes first decides: M present -> the
+// two-block chain; M not started yet -> the squarer runs the last chunk alone
+// (ds_fe_last, the same value) and a late M finds kRoleSolo and returns.  Neither
+// side ever waits on a block that is not running.
+constexpr int kRoleWord = 1000;
+constexpr uint32_t kRoleM = 1, kRoleSolo = 2;
+static_assert(kRoleWord >= kMaxSeg && kRoleWord < kDsChanOff, "role word between the zero flags and the channel");
+__device__ __forceinline__ uint32_t tail_claim(uint32_t* zf, uint32_t role) {  // thread 0; returns the word's old value
+    uint32_t expect = 0;
+    __hip_atomic_compare_exchange_strong((__attribute__((address_space(1))) uint32_t*)(zf + kRoleWord), &expect, role,
+                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return expect;
+}
+__shared__ uint32_t g_tail_role;
 __global__ void __launch_bounds__(kTailThreads) k_seg_fe1(uint32_t* __restrict__ g, SegPlan plan,
                                                           uint32_t* __restrict__ zf) {
     fold_table_init();
     const WL w = wl();
     const int s = (int)blockIdx.x;
-    {  // k_horner_tree2's channel: every stamp cleared (the blocks share the words)
+    {  // k_horner_tree2's channel: every stamp cleared (the blocks share the words), the role word too
         uint64_t* ch = (uint64_t*)(zf + kDsChanOff);
         for (int i = s * kTailThreads + (int)threadIdx.x; i < kDsChanWords / 2; i += plan.S * kTailThreads)
             __hip_atomic_store(ch + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s == 0 && threadIdx.x == 0)
+            __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)(zf + kRoleWord), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     int e = 0;
     for (int t = s + 1; t < plan.S; ++t) e += plan.hi[t] - plan.lo[t];
@@ -235,8 +260,14 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
     }
 #if BN_TAIL_DS
     if (do_fe && zf && blockIdx.x == 1) {  // the multiplier block of the final exponentiation
+#if BN_TAIL_LATE_M  // test build (`make chanfail`): M starts ~2 ms late, so the squarer must go on alone
+        for (int t = 0; t < 40000; ++t) __builtin_amdgcn_s_sleep(1);
+#endif
+        if (threadIdx.x == 0) g_tail_role = tail_claim(const_cast<uint32_t*>(zf), kRoleM);
+        __syncthreads();
+        if (g_tail_role != 0) return;  // the squarer block has gone on alone
         ds_init();
-        DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0};
+        DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0, false};
         ds_fe_last_m(ch);
         return;
     }
@@ -286,8 +317,14 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
         if (zero && err && threadIdx.x == 0) err_or(err, BN_ERR_FE_ZERO);
         ds_init();
         uint32_t d = ds_from_w12(x);
-        if (zf && gridDim.x == 2) {  // with the multiplier block (block 1)
-            DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0};
+        bool duo = false;
+        if (zf && gridDim.x == 2) {  // with the multiplier block (block 1), if it has started
+            if (threadIdx.x == 0) g_tail_role = tail_claim(const_cast<uint32_t*>(zf), kRoleSolo);
+            __syncthreads();
+            duo = g_tail_role == kRoleM;
+        }
+        if (duo) {
+            DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0, false};
             d = ds_fe_last_s(d, ch);
         } else {
             d = ds_fe_last(d);

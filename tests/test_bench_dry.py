@@ -21,7 +21,7 @@ def run(args, env=None):
                           timeout=240, env=e, cwd=ROOT)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_spawns_ranks_config4(world):
     r = run(["--gpus", str(world), "--dry-run-cpu", "--steps", "1", "--warmup", "1", "--total", "16384",
              "--chunk", "2048"])
@@ -59,7 +59,7 @@ def test_bench_world_size_must_match_gpus():
     assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr
 
 
-@pytest.mark.parametrize("ndev", [1, 3])
+@pytest.mark.parametrize("ndev", [1, 3, 8])
 def test_bench_capi_form_keys(ndev):
     """`--form capi`: config 4 in one process over N devices (bn_ctx_create_multi +
     bn_pairing_many_allgather_dev on the GPU); here the stub engine: no ranks are
@@ -88,3 +88,28 @@ def test_bench_capi_form_rejects_launcher_and_workloads():
     r = run(["--workload", "g2mul", "--gpus", "2", "--dry-run-cpu"], env={"WORLD_SIZE": "2", "RANK": "0",
                                                                       "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "runs on one GPU" in r.stderr
+
+
+def test_bench_under_the_drivers_launcher_world8():
+    """The driver's own N = 8 command line (torch.distributed.run with eight ranks on
+    127.0.0.1, bench.py --gpus 8 in every rank), with the stub engine on gloo: the
+    exact control flow of SCALE's 8-GPU point."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "8", "--steps", "1", "--warmup", "1", "--dry-run-cpu", "--total", "16384",
+                        "--chunk", "2048"], capture_output=True, text=True, timeout=300, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 alone prints the line
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 8 and line["config"]["pairs_per_gpu"] == 2048
+    assert line["cross_rank_check"]["ranks_ok"] == 8 and line["collective"]["world_from_allreduce"] == 8
+    assert line["sample_check"]["mismatches"] == 0

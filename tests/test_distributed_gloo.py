@@ -1,4 +1,4 @@
-"""World-size-2 gloo tests of the multi-GPU path (substrate_bn/parallel.py) on
+"""World-size-2 and -8 gloo tests of the multi-GPU path (substrate_bn/parallel.py) on
 CPU: sharding, the variable-length all-gather of Gt results, and the
 rank-ordered partial-product exchange of pairing_batch.  The per-shard compute
 is injected (the oracle stands in for the GPU engine here; it is only the
@@ -57,17 +57,19 @@ def worker(rank, world, port, n, qout):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [7, 2])
-def test_world2_sharding_and_gather(n):
+@pytest.mark.parametrize("world,n", [(2, 7), (2, 2), (8, 13), (8, 5)])
+def test_world_sharding_and_gather(world, n):
+    """World 8 is config 4's rank count: 13 pairs give shards of
+    one and two, 5 pairs leave three ranks with an empty shard."""
     from oracle import oracle as O
     ctx = mp.get_context("spawn")
     qout = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, 2, port, n, qout)) for r in range(2)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, qout)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = {}
-    for _ in range(2):
+    for _ in range(world):
         rank, many, prod = qout.get(timeout=120)
         assert many is not None, prod
         res[rank] = (many, prod)
@@ -80,7 +82,7 @@ def test_world2_sharding_and_gather(n):
         p[2, 4:8] = O.canon_to_mont_array([1])
     want_many = O.pairing_many(p, q, 2)
     want_prod = O.pairing_batch(p, q)
-    for r in (0, 1):
+    for r in range(world):
         assert np.array_equal(res[r][0], want_many)
         assert np.array_equal(res[r][1], want_prod)
 

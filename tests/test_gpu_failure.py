@@ -40,9 +40,11 @@ def test_capped_handoff_fails_the_call():
     assert res["pairing_batch"] == BN_ERR_INTERNAL and not res["pairing_batch_value_returned"], res
     assert res["miller_loop_batch"] == BN_ERR_INTERNAL, res
     assert res["final_exponentiation_many"] == BN_ERR_INTERNAL, res
-    # the segmented product (4,224 terms): the digit-sliced tail's two-block channel
+    # the segmented product (4,224 terms): the digit-sliced tail's two-block channel,
+    # failing promptly (within 1 s)
     assert res["pairing_batch_segmented"] == BN_ERR_INTERNAL, res
     assert not res["pairing_batch_segmented_value_returned"], res
+    assert res["pairing_batch_segmented_s"] < 1.0, res
     # the status-less device call is accepted, and bn_dev_status reports the failure once
     assert res["pairing_many_dev_call"] == BN_OK, res
     assert res["dev_status_after"] == BN_ERR_INTERNAL, res
@@ -52,3 +54,33 @@ def test_capped_handoff_fails_the_call():
     assert res["pairing_batch_dev_status"] == BN_ERR_INTERNAL, res
     # the throughput kernel has no capped waits: the same library is still bit-exact there
     assert res["throughput_path"] == BN_OK and res["throughput_path_bit_exact"], res
+
+
+def _tail_probe(lib):
+    path = os.path.join(ROOT, "paritytech-bn_amd", lib)
+    assert os.path.exists(path), "%s not built: make -C paritytech-bn_amd chanfail latem" % lib
+    env = dict(os.environ, BN254MI_LIB=path)
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "failure_probe.py")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_tail_channel_fails_fast_after_one_expired_wait():
+    """Every store of the squarer <-> multiplier channel dropped, at a spin cap of 2^20
+    polls (~60 ms per expired wait): without the channel's sticky `dead` flag
+    (fq12_ds.h ds_chan_ld) the multiplier's 80 takes and the squarer's 5 result
+    reads would each spin out, ~5 s; with it each wave spins out once."""
+    res = _tail_probe("libbn254mi_chanfail.so")
+    assert res["code"] == BN_ERR_INTERNAL and not res["value_returned"], res
+    assert res["seconds_1"] < 1.5, res
+
+
+@pytest.mark.gpu
+def test_tail_squarer_goes_on_alone_when_the_multiplier_is_late():
+    """The multiplier block of k_horner_tree2 starting ~2 ms late (as when other work
+    holds the CUs): the squarer claims the last chunk alone (kernels_tail.hip role
+    word), the late block returns, and the product is bit-exact."""
+    res = _tail_probe("libbn254mi_latem.so")
+    assert res["code"] == BN_OK and res["value_returned"] and res["bit_exact"], res

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build an A/B variant of libbn254mi.so with extra compile flags into
-# exp/lib_NAME.so (bench.py / tests load it with BN254MI_LIB=ab/lib_NAME.so).
+# ab/lib_NAME.so (bench.py / tests load it with BN254MI_LIB=ab/lib_NAME.so).
 # Usage: tools/build_variant.sh NAME "-DFLAG=1 ..."
 set -e
 NAME=$1; FLAGS=$2

@@ -20,6 +20,8 @@ timeout -k 10 300 python -u bench.py --form capi --gpus ${CAPI_GPUS:-1} --steps 
 head -c 400 $OUT/bench_capi.json; echo
 echo "== kernel stats"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python3 bench.py $Q > $OUT/bench_prof.json 2> $OUT/prof.err
+# per-kernel CSV with the steady-state columns (SteadyAverageNs: without the cold first launch; MedianNs)
+python3 tools/rocpd_stats.py $(find $OUT/prof -name '*results.db' | head -1) > $OUT/kernel_stats.csv || true
 echo "== pmc"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_fetch.err
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o p -- python3 bench.py --steps 2 --warmup 1 $Q > /dev/null 2> $OUT/pmc_write.err
@@ -43,6 +45,7 @@ for w in g1mul g2mul product gtpow g2validate g2decompress; do
   head -c 300 $OUT/bench_$w.json; echo
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_product -o run -- python3 bench.py --workload product --steps 10 > /dev/null 2> $OUT/prof_product.err
+python3 tools/rocpd_stats.py $(find $OUT/prof_product -name '*results.db' | head -1) > $OUT/product_kernel_stats.csv || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_g1mul -o run -- python3 bench.py --workload g1mul --steps 5 --cpu-sample 64 > /dev/null 2> $OUT/prof_g1mul.err
 if [ -f exp/lib_mulstats.so ]; then
   echo "== G*Fr schedule counters (diagnostic build)"
