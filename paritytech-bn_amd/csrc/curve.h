@@ -11,8 +11,10 @@
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #define BN_ANY(p) (__any((int)(p)) != 0)
+#define BN_ALL(p) (__all((int)(p)) != 0)
 #else
 #define BN_ANY(p) (p)
+#define BN_ALL(p) (p)
 #endif
 
 namespace bn {

@@ -269,6 +269,12 @@ __device__ __forceinline__ void st_words(bn_fq* dst, const uint32_t w[8]) {
 __device__ __forceinline__ bool words_zero(const uint32_t w[8]) {
     return (w[0] | w[1] | w[2] | w[3] | w[4] | w[5] | w[6] | w[7]) == 0;
 }
+// the reference's Montgomery image of one (R mod p, little-endian 32-bit words): the
+// value `z == one` compares against in to_affine (mod.rs:199-216)
+__device__ __forceinline__ bool words_one(const uint32_t w[8]) {
+    return ((w[0] ^ 0xc58f0d9du) | (w[1] ^ 0xd35d438du) | (w[2] ^ 0xf5c70b3du) | (w[3] ^ 0x0a78eb28u) |
+            (w[4] ^ 0x7879462cu) | (w[5] ^ 0x666ea36fu) | (w[6] ^ 0x9a07df2fu) | (w[7] ^ 0x0e0a77c1u)) == 0;
+}
 __device__ __forceinline__ Fq<2> ld_ref(const bn_fq& a) {
     uint32_t w[8];
     ld_words(&a, w);

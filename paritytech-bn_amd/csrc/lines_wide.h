@@ -26,12 +26,15 @@ __device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p
     uint32_t w[8];
     ld_words(&p[i].z, w);
     const bool p_zero = words_zero(w);
+    const bool p_one = words_one(w);
     const Fq<2> pz = fq_load_ref(w);
 #if BN_SPLIT
     uint32_t wz[8];
     ld_words(lane_odd() ? &q[i].z.c1 : &q[i].z.c0, wz);  // this lane's coordinate of z
     const uint32_t own_zero = words_zero(wz) ? 1u : 0u;
     const bool q_zero = (own_zero & swap_pair(own_zero)) != 0;
+    const uint32_t own_one = (lane_odd() ? words_zero(wz) : words_one(wz)) ? 1u : 0u;  // z = one + 0 u
+    const bool q_one = (own_one & swap_pair(own_one)) != 0;
     const Fq2<2> qz = {fq_load_ref(wz)};
     const auto qz_sq = fq_sqr(qz.c);
     const auto nq = fq_add(qz_sq, fq_partner(qz_sq));  // N(qz) = z0^2 + z1^2, the same on both lanes
@@ -40,6 +43,7 @@ __device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p
     ld_words(&q[i].z.c0, w0);
     ld_words(&q[i].z.c1, w1);
     const bool q_zero = words_zero(w0) && words_zero(w1);
+    const bool q_one = words_one(w0) && words_zero(w1);
     const Fq2<2> qz = {fq_load_ref(w0), fq_load_ref(w1)};
     const auto nq = fq_add(fq_sqr(qz.c0), fq_sqr(qz.c1));
 #endif
@@ -51,7 +55,16 @@ __device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p
     // and qz^-1 = conj(qz) * (t * pz).  Inverses are unique: these are the values the
     // reference's two inversions give.  A zero z makes t = 0; that pair is skipped
     // (flags) or rejected (mode 1) and its values are never used.
-    const Fq<2> t = fq_inv(fq_mul(pz, nq));
+    // The reference's z == one branch (mod.rs:199-216: the affine point is (x, y) itself):
+    // when every pair of the wave has both z == one (points that came in affine, e.g.
+    // through AffineG1::new / AffineG2::new), t = (1 * 1)^-1 = 1 needs no inversion --
+    // the binary GCD is ~25 k VALU per wave, ~17 % of k_prepare_wide.  The products
+    // below then multiply by one: the same values.
+    Fq<2> t;
+    if (BN_ALL(p_one && q_one))  // wave-uniform
+        t = widen<2>(fq_one());
+    else
+        t = fq_inv(fq_mul(pz, nq));
     const auto pzinv = fq_mul(t, nq);
     const auto ninv = fq_mul(t, pz);
     auto pzinv2 = fq_sqr(pzinv);

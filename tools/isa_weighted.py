@@ -39,11 +39,13 @@ def main():
     bl = blocks(path, sym)
     tot = collections.Counter()
     seen = collections.Counter()
+    per_op = {}
     for name, b in bl:
         c = collections.Counter(cls(x) for x in b)
         w, tag = table.get(c["mad64"], (1.0, None)) if c["mad64"] else (1.0, None)
         if tag:
             seen[tag] += 1
+            per_op.setdefault(tag, (name, c))
         for k, v in c.items():
             tot[k] += v * w
     valu = {k: v for k, v in tot.items() if k in sum(GROUPS.values(), []) or k.startswith("valu_")}
@@ -56,6 +58,16 @@ def main():
     n = sum(rest.values())
     print("  %-62s %9.0f  %5.1f %%  %s" % ("other VALU", n, 100 * n / allv,
                                           ", ".join("%s=%.0f" % kv for kv in sorted(rest.items(), key=lambda x: -x[1])[:6])))
+    # per matched operation: its block's VALU, VALU per MAD and category split (one execution)
+    short = ["mad64", "carry/norm", "add/sub", "dpp/mov", "select", "mul_lo/fold"]
+    print("\n  per operation (one execution of its block):")
+    print("  %-14s %-10s %8s %8s %6s  %s" % ("op", "block", "VALU", "MAD", "V/MAD", "  ".join("%10s" % s for s in short)))
+    for tag, (name, c) in per_op.items():
+        v = {k: x for k, x in c.items() if k in sum(GROUPS.values(), []) or k.startswith("valu_")}
+        nv = sum(v.values())
+        cats = [sum(v.get(k, 0) for k in ks) for ks in GROUPS.values()]
+        print("  %-14s %-10s %8d %8d %6.2f  %s" % (tag, name, nv, c["mad64"], nv / max(1, c["mad64"]),
+                                                  "  ".join("%9.1f%%" % (100.0 * x / nv) for x in cats)))
 
 
 if __name__ == "__main__":
