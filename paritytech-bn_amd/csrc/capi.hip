@@ -637,6 +637,12 @@ static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out
             HIPCHK(c, hipGetLastError());
             zf = z;
         }
+        // two blocks: the squarer (block 0) and the multiplier (block 1) of the last
+        // chunk hand values over by polling global memory, which needs both resident.
+        // HIP does not promise co-residency, so the blocks claim their roles through a
+        // word k_seg_fe1 clears (kernels_tail.hip tail_claim): a multiplier that has not
+        // started when the squarer gets there is not waited for -- the squarer runs
+        // the chunk alone (the same value) and the late block returns.
         k_horner_tree2<<<zf && BN_TAIL_M ? 2 : 1, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err,
                                                           zf);
     }

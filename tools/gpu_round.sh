@@ -34,6 +34,9 @@ timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_g1_write -o p -- pyth
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_g1_sq -o p -- python3 bench.py --workload g1mul --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_g1_sq.err
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_g2_sq -o p -- python3 bench.py --workload g2mul --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_g2_sq.err
 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_prod_sq -o p -- python3 bench.py --workload product --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_prod_sq.err
+# config 5 with the two-lane line producer (k_prepare, BN254MI_PREPARE_WIDE_MAX=0): its waves' VALU and lifetime
+# (the chain a streamed two-lane producer would put in front of the segmented Miller loop)
+BN254MI_PREPARE_WIDE_MAX=0 timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/pmc_prod2_sq -o p -- python3 bench.py --workload product --steps 2 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/pmc_prod2_sq.err
 if [ -f paritytech-bn_amd/libbn254mi_dbg.so ]; then
   echo "== fold check (libbn254mi_dbg.so: every fold site counts bound violations)"
   BN254MI_LIB=paritytech-bn_amd/libbn254mi_dbg.so timeout -k 10 300 python -u tools/fold_check.py 4096 > $OUT/fold_check.json 2> $OUT/fold_check.err || { tail -20 $OUT/fold_check.err; exit 1; }
