@@ -434,7 +434,24 @@ static int seg_lines(int d, int e) {  // (digits + nonzero digits in [d, e), by 
 // (weights from the ISA -- 5,338 VALU per squaring against 4,730 plus the loads per
 // line -- and three settings between them planned no better on the GPU,
 // profiles/r5e_ab_segment_plan.txt)
-constexpr int kSegWSq = 36, kSegWLine = 39;
+constexpr int kSegWSqDefault = 36, kSegWLineDefault = 39;
+// BN254MI_SEG_WEIGHTS="sq,line" overrides the two weights (A/B of the plan's cost model)
+static int seg_weight(int which) {
+    struct W {
+        int v[2];
+    };
+    static const W w = [] {  // read once (thread-safe static initialization)
+        W r = {{kSegWSqDefault, kSegWLineDefault}};
+        if (const char* e = getenv("BN254MI_SEG_WEIGHTS")) {
+            int x = 0, y = 0;
+            if (sscanf(e, "%d,%d", &x, &y) == 2 && x > 0 && y > 0) r = {{x, y}};
+        }
+        return r;
+    }();
+    return w.v[which];
+}
+#define kSegWSq seg_weight(0)
+#define kSegWLine seg_weight(1)
 static int seg_cost(int d, int e, int K) { return kSegWSq * seg_sq(d, e) + kSegWLine * K * seg_lines(d, e); }
 static void plan_index(SegPlan& p) {
     for (int k = 0; k < p.S; ++k)

@@ -186,10 +186,28 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* 
 // A pair with a zero point (flags) or past n contributes the line one
 // (ell_0 = 1, ell_vw = ell_vv = 0): the sparse product by it is f itself.
 // Launched with kPairBlock threads per block (kernels.h: issue balance).
+#ifndef BN_SEG_STAMPS
+#define BN_SEG_STAMPS 0
+#endif
+#if BN_SEG_STAMPS
+// diagnostic build (tools/build_variant.sh segstamps -DBN_SEG_STAMPS=1, tools/seg_stamps.py):
+// lane 0 of every wave of k_miller_seg records s_memrealtime (100 MHz) when the wave
+// starts and ends, and its segment: where the kernel's wave lifetime goes
+constexpr int kSegStampWaves = 4096;
+__device__ uint64_t g_seg_stamps[kSegStampWaves][4];
+#define SEG_STAMP(slot, v)                                                                  \
+    do {                                                                                    \
+        const size_t w_ = lane_id() / 64;                                                   \
+        if ((threadIdx.x & 63u) == 0 && w_ < (size_t)kSegStampWaves) g_seg_stamps[w_][slot] = (v); \
+    } while (0)
+#else
+#define SEG_STAMP(slot, v) ((void)0)
+#endif
 __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const uint32_t* __restrict__ coeffs,
                                                                        const uint32_t* __restrict__ paff,
                                                                        const uint8_t* __restrict__ flags, size_t n,
                                                                        SegPlan plan, uint32_t* __restrict__ out) {
+    SEG_STAMP(0, __builtin_amdgcn_s_memrealtime());
     fold_table_init();
     const Balance bal = balance_init();
     const size_t l = lane_id(), lp = l / kL, nl = kL * n;
@@ -198,6 +216,8 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
     while (s + 1 < plan.S && lp >= (size_t)plan.off[s + 1]) ++s;
     const size_t K = (size_t)plan.K[s], G = plan.G[s];
     const size_t g = lp - plan.off[s], c = l % kL;
+    SEG_STAMP(2, (uint64_t)s);
+    SEG_STAMP(3, (uint64_t)K);
     if (g >= G) return;
     const Ell one_line = {widen<kLine>(fq2_one()), widen<kLine>(fq2_zero()), widen<kLine>(fq2_zero())};
     // line k of pair t of this group, with the pair's affine P
@@ -245,6 +265,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
         }
     }
     st_fq12(out, kL * (size_t)plan.total, l, f);
+    SEG_STAMP(1, __builtin_amdgcn_s_memrealtime());
 }
 
 // G2 * Fr (mod.rs:272-292) on the pairing path's two-lane layout: the chain of
@@ -272,3 +293,11 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_g2_mul_split(const 
 }  // namespace bn
 
 BN_EXPORT_FOLD_CHECK(pairing)
+
+#if BN_SEG_STAMPS
+extern "C" int bn_dbg_seg_stamps(uint64_t* out, int nwaves) {
+    if (nwaves > bn::kSegStampWaves) nwaves = bn::kSegStampWaves;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(bn::g_seg_stamps), (size_t)nwaves * 4 * sizeof(uint64_t)) == hipSuccess
+               ? nwaves : -1;
+}
+#endif
