@@ -189,6 +189,9 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* 
 #ifndef BN_SEG_STAMPS
 #define BN_SEG_STAMPS 0
 #endif
+#ifndef BN_SEG_LINE_BALANCE
+#define BN_SEG_LINE_BALANCE 1
+#endif
 #if BN_SEG_STAMPS
 // diagnostic build (tools/build_variant.sh segstamps -DBN_SEG_STAMPS=1, tools/seg_stamps.py):
 // lane 0 of every wave of k_miller_seg records s_memrealtime (100 MHz) when the wave
@@ -246,9 +249,16 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
     const int end = hi == BN_NAF_DIGITS ? BN_NAF_DIGITS + 2 : hi;
     int idx = plan.idx[s];
     Fq12<kF> f = widen<kF>(fq12_one());
+    // Issue balance (kernels.h) at every line, not only every digit: a segment is 3-8
+    // digits of up to 16 K-pair lines each, and with one position per digit the
+    // older wave of a SIMD ran up to a digit ahead of its partner and finished
+    // ~150 us earlier, the younger one then running its last digit alone
+    // (tools/seg_stamps.py: wave durations 370-520 us inside every segment, wave
+    // life 0.72-0.84).  Positions: digit * 256, then 1 + pass * 64 + t per line (K <= 64).
 #pragma unroll 1
     for (int i = lo; i < end; ++i) {
-        balance_step(bal, (uint32_t)(i - lo));
+        const uint32_t dpos = (uint32_t)(i - lo) << 8;
+        balance_step(bal, dpos);
         const bool closing = i >= BN_NAF_DIGITS;
         if (!closing && i > lo) f = narrow12<kF>(fq12_sqr(f));
         const int passes = closing ? 1 : 1 + (int)((kNafNonzero >> i) & 1u);
@@ -256,6 +266,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
         for (int ps = 0; ps < passes; ++ps, ++idx) {
 #pragma unroll 1
             for (size_t t = 0; t < K; ++t) {
+                if (BN_SEG_LINE_BALANCE) balance_step(bal, dpos + 1u + ((uint32_t)ps << 6) + (uint32_t)t);
                 const PairLine pl = pair_line(t, idx);
                 if (i == lo && ps == 0 && t == 0)
                     f = line_from_one(pl.e, pl.px, pl.py);  // one * line (mod.rs:589 on f = one)
