@@ -613,14 +613,30 @@ __device__ __forceinline__ void ds_put_result(DsChan& ch, uint32_t a) {  // M
 __device__ __forceinline__ uint32_t ds_get_result(DsChan& ch) {  // S
     return ds_chan_ld(ch.w + 128 * (kDsItems + ch.results++), ch);
 }
+// Diagnostic (-DBN_TAIL_STAMPS=1, tools/tail_stamps.py): thread 0 of a block records
+// s_memrealtime (100 MHz) at the phase boundaries of the product's tail
+// (k_seg_fe1's segment 0, and k_horner_tree2's squarer and multiplier blocks)
+#ifndef BN_TAIL_STAMPS
+#define BN_TAIL_STAMPS 0
+#endif
+#if BN_TAIL_STAMPS
+__device__ uint64_t g_tail_stamps[32];
+#define TAIL_STAMP(i)                                                                      \
+    do {                                                                                   \
+        if (threadIdx.x == 0) g_tail_stamps[i] = __builtin_amdgcn_s_memrealtime();       \
+    } while (0)
+#else
+#define TAIL_STAMP(i) ((void)0)
+#endif
 // S's side of exp_by_neg_z: x^(2^k) handed over at each nonzero NAF digit of u
-__device__ __noinline__ uint32_t ds_exp_sq(uint32_t xx, DsChan& ch) {
+__device__ __noinline__ uint32_t ds_exp_sq(uint32_t xx, DsChan& ch, int stamp = -1) {
 #pragma unroll 1
     for (int k = 0;; ++k) {
         if ((kZNaf.nz >> k) & 1u) ds_put(ch, xx);
         if (k == kZNaf.top) break;
         xx = ds_cyc(xx);
     }
+    if (BN_TAIL_STAMPS && stamp >= 0) TAIL_STAMP(stamp);  // the squarings are done; M's product is awaited
     return ds_get_result(ch);
 }
 // M's side: the product of the handed-over powers (x^-1 = conj(x) in the cyclotomic
@@ -642,14 +658,17 @@ __device__ __noinline__ uint32_t ds_exp_mul(DsChan& ch) {
 // returns a, e, g, then o = frob(k b) and u = frob^3(conj(s) k b) (fq12_wide.h
 // w12_fe_last_s / w12_final_exp_m, the reference's names)
 __device__ __noinline__ uint32_t ds_fe_last_s(uint32_t s, DsChan& ch) {
-    const uint32_t a = ds_exp_sq(s, ch);
+    const uint32_t a = ds_exp_sq(s, ch, 2);
+    TAIL_STAMP(3);
     const uint32_t b = ds_cyc(a);
     ds_put(ch, b);
     const uint32_t c = ds_cyc(b);
     const uint32_t d = ds_mul(c, b, false);
-    const uint32_t e = ds_exp_sq(d, ch);
+    const uint32_t e = ds_exp_sq(d, ch, 4);
+    TAIL_STAMP(5);
     const uint32_t f1 = ds_cyc(e);
-    const uint32_t g = ds_exp_sq(f1, ch);
+    const uint32_t g = ds_exp_sq(f1, ch, 6);
+    TAIL_STAMP(7);
     const uint32_t j = ds_mul(e, g, true);  // conj(g) * e
     const uint32_t k = ds_mul(j, d, true);  // j * conj(d)
     ds_put(ch, k);

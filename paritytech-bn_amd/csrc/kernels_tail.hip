@@ -29,6 +29,10 @@
 #if BN_TAIL_DS
 #include "fq12_ds.h"
 #endif
+#ifndef TAIL_STAMP  // (fq12_ds.h defines the diagnostic stamps; BN_TAIL_DS=0 builds have none)
+#define BN_TAIL_STAMPS 0
+#define TAIL_STAMP(i) ((void)0)
+#endif
 
 namespace bn {
 
@@ -220,17 +224,20 @@ __global__ void __launch_bounds__(kTailThreads) k_seg_fe1(uint32_t* __restrict__
         const bool zero = w12_is_zero(x);
         if (threadIdx.x == 0) zf[s] = zero ? 1u : 0u;
     }
+    if (BN_TAIL_STAMPS && s == 0) TAIL_STAMP(16);
 #if BN_FE1_PAR
     x = w12_fe_first_par(x);  // group 0 gets the first chunk
 #else
     if (threadIdx.x < (unsigned)kWLanes) x = w12_fe_first(x);
 #endif
+    if (BN_TAIL_STAMPS && s == 0) TAIL_STAMP(17);
     ds_init();
     uint32_t d = ds_from_w12(x);
 #pragma unroll 1
     for (int k = 0; k < e; ++k) d = ds_cyc(d);
     x = ds_to_w12(d);
     if (threadIdx.x < 12) w_st_split(g, (size_t)plan.S, (size_t)s, w, x);
+    if (BN_TAIL_STAMPS && s == 0) TAIL_STAMP(18);
 }
 #endif
 
@@ -244,6 +251,7 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
                                                                int do_fe, bn_gt* __restrict__ out,
                                                                int* __restrict__ err,
                                                                const uint32_t* __restrict__ zf) {
+    if (BN_TAIL_STAMPS) TAIL_STAMP(blockIdx.x == 0 ? 0 : 24);
     if (threadIdx.x == 0) g_tail_zero = 0;
     if (threadIdx.x < kTailDuo * 4) g_tail_cnt[threadIdx.x] = 0;
     __syncthreads();  // the resets are seen before any group can use them
@@ -266,9 +274,11 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
         if (threadIdx.x == 0) g_tail_role = tail_claim(const_cast<uint32_t*>(zf), kRoleM);
         __syncthreads();
         if (g_tail_role != 0) return;  // the squarer block has gone on alone
+        if (BN_TAIL_STAMPS) TAIL_STAMP(25);
         ds_init();
         DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0, false};
         ds_fe_last_m(ch);
+        if (BN_TAIL_STAMPS) TAIL_STAMP(26);
         return;
     }
 #endif
@@ -315,6 +325,7 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
     if (do_fe) {
         const bool zero = g_tail_zero != 0;
         if (zero && err && threadIdx.x == 0) err_or(err, BN_ERR_FE_ZERO);
+        if (BN_TAIL_STAMPS) TAIL_STAMP(1);
         ds_init();
         uint32_t d = ds_from_w12(x);
         bool duo = false;
@@ -329,6 +340,7 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
         } else {
             d = ds_fe_last(d);
         }
+        if (BN_TAIL_STAMPS) TAIL_STAMP(8);
         const Fq<2> r = ds_to_w12(d);  // every thread; threads 0..11 get the value
         if (!zero && threadIdx.x < 12) fq_store_ref(r, words);
     } else {
@@ -359,3 +371,9 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
 }  // namespace bn
 
 BN_EXPORT_FOLD_CHECK(tail)
+
+#if BN_TAIL_STAMPS
+extern "C" int bn_dbg_tail_stamps(uint64_t out[32]) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(bn::g_tail_stamps), 32 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
