@@ -340,7 +340,7 @@ __device__ __forceinline__ uint64_t ds_col(const uint32_t (&u)[10], const uint32
 // Granger-Scott cyclotomic squaring (fq12.rs:198-247, as fq12_wide.h w12_cyc):
 // slot (e, c), e < 3: P_e = x y of pair e = (w^e, w^(e+3)); e >= 3: Q = (x + y)(xi y + x)
 // of pair e - 3; then every output coordinate from them (kDsComb)
-__device__ __noinline__ uint32_t ds_cyc(uint32_t a) {
+__device__ __forceinline__ uint32_t ds_cyc_body(uint32_t a) {
     DS_STAMP_INIT;
     const DsLane x = ds_lane();
     const int wk = ds_wk(x);
@@ -387,6 +387,11 @@ __device__ __noinline__ uint32_t ds_cyc(uint32_t a) {
     DS_STAMP(6);
     return r;
 }
+// the out-of-line form (most call sites); the squaring chains of the tail (ds_exp_sq,
+// k_seg_fe1's squarings) inline ds_cyc_body: a call saves and reloads registers through
+// scratch, and the reload's s_waitcnt vmcnt also waits for the hand-off stores issued
+// before it (gfx950 counts stores in vmcnt)
+__device__ __noinline__ uint32_t ds_cyc(uint32_t a) { return ds_cyc_body(a); }
 
 // a * b (fq12.rs:319-327) on the w-basis: out_e = sum_i a'_i b_(e - i mod 6) with
 // a'_i = xi a_i where the index wraps (w^6 = xi); conj_b: b's conjugate (its odd
@@ -629,19 +634,24 @@ __device__ uint64_t g_tail_stamps[32];
 #define TAIL_STAMP(i) ((void)0)
 #endif
 // S's side of exp_by_neg_z: x^(2^k) handed over at each nonzero NAF digit of u
-__device__ __noinline__ uint32_t ds_exp_sq(uint32_t xx, DsChan& ch, int stamp = -1) {
+// (force-inlined, as ds_exp_mul and the two last-chunk drivers below: the channel state
+// then lives in registers; as __noinline__ functions they took DsChan by reference, i.e.
+// through the stack, and every put and take paid two scratch round trips behind an
+// s_waitcnt vmcnt(0) that also waited for the previous put's store -- S's squarings ran
+// 1.39 us each against 1.17 us without hand-offs, tools/tail_stamps.py)
+__device__ __forceinline__ uint32_t ds_exp_sq(uint32_t xx, DsChan& ch, int stamp = -1) {
 #pragma unroll 1
     for (int k = 0;; ++k) {
         if ((kZNaf.nz >> k) & 1u) ds_put(ch, xx);
         if (k == kZNaf.top) break;
-        xx = ds_cyc(xx);
+        xx = ds_cyc_body(xx);
     }
     if (BN_TAIL_STAMPS && stamp >= 0) TAIL_STAMP(stamp);  // the squarings are done; M's product is awaited
     return ds_get_result(ch);
 }
 // M's side: the product of the handed-over powers (x^-1 = conj(x) in the cyclotomic
 // subgroup); returns the first item (x itself)
-__device__ __noinline__ uint32_t ds_exp_mul(DsChan& ch) {
+__device__ __forceinline__ uint32_t ds_exp_mul(DsChan& ch) {
     const uint32_t x0 = ds_take(ch);
     uint32_t acc = (kZNaf.minus & 1u) ? ds_conj(x0) : x0;
 #pragma unroll 1
@@ -657,7 +667,7 @@ __device__ __noinline__ uint32_t ds_exp_mul(DsChan& ch) {
 // hand-overs are [24 powers of s], b, [24 powers of d], [24 powers of f1], k; M
 // returns a, e, g, then o = frob(k b) and u = frob^3(conj(s) k b) (fq12_wide.h
 // w12_fe_last_s / w12_final_exp_m, the reference's names)
-__device__ __noinline__ uint32_t ds_fe_last_s(uint32_t s, DsChan& ch) {
+__device__ __forceinline__ uint32_t ds_fe_last_s(uint32_t s, DsChan& ch) {
     const uint32_t a = ds_exp_sq(s, ch, 2);
     TAIL_STAMP(3);
     const uint32_t b = ds_cyc(a);
@@ -681,7 +691,7 @@ __device__ __noinline__ uint32_t ds_fe_last_s(uint32_t s, DsChan& ch) {
     const uint32_t u = ds_get_result(ch);
     return ds_mul(u, r, false);
 }
-__device__ __noinline__ void ds_fe_last_m(DsChan& ch) {
+__device__ __forceinline__ void ds_fe_last_m(DsChan& ch) {
     const uint32_t s = ds_exp_mul(ch);  // a
     const uint32_t b = ds_take(ch);
     (void)ds_exp_mul(ch);               // e

@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(kTailThreads) k_seg_fe1(uint32_t* __restrict__
     ds_init();
     uint32_t d = ds_from_w12(x);
 #pragma unroll 1
-    for (int k = 0; k < e; ++k) d = ds_cyc(d);
+    for (int k = 0; k < e; ++k) d = ds_cyc_body(d);
     x = ds_to_w12(d);
     if (threadIdx.x < 12) w_st_split(g, (size_t)plan.S, (size_t)s, w, x);
     if (BN_TAIL_STAMPS && s == 0) TAIL_STAMP(18);
