@@ -329,12 +329,13 @@ BN_INLINE auto fq2_conj(const Fq2<B>& a) {
     const Fq<kv(B)> own = fq_norm(a.c);
     return wrap2(fq_select(lane_odd(), fq_neg(own), own));
 }
-// fq2.rs:119-130: t = (c0^2 + c1^2)^-1 on both lanes, then (c0 t, -c1 t)
-template <int B>
+// fq2.rs:119-130: t = (c0^2 + c1^2)^-1 on both lanes, then (c0 t, -c1 t); Quad: both
+// lane pairs of every quad hold the same element (fq_inv_quad)
+template <bool Quad = false, int B>
 BN_INLINE auto fq2_inv(const Fq2<B>& a_in) {
     auto a = pre<40>(a_in);
     const auto sq = fq_sqr(a.c);
-    const auto t = fq_inv(fq_add(sq, fq_partner(sq)));  // the same norm on both lanes
+    const auto t = fq_inv<Quad>(fq_add(sq, fq_partner(sq)));  // the same norm on both lanes
     const auto r = fq_mul(a.c, t);
     return wrap2(fq_select(lane_odd(), fq_neg(r), r));
 }

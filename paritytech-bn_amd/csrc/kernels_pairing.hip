@@ -53,7 +53,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_prepare_wide(const 
     const size_t lt = i * kL + (l & 1);  // this lane's index in k_prepare's per-pair arrays
     const int k = pw_slot();
     const bool st = k == 0;
-    const PairAffine a = pair_to_affine(p, q, i, lt, flags, err, st ? mode : 0);
+    const PairAffine a = pair_to_affine<true>(p, q, i, lt, flags, err, st ? mode : 0);
     if (st) {
         st_fq(paff, nl, lt, 0, a.px);
         st_fq(paff, nl, lt, 1, a.py);

@@ -135,7 +135,7 @@ __device__ __noinline__ void inv_fq6_par() {
     inv_round(Cr);
     {  // t = n0 C0 + xi (n2 C1 + n1 C2), t^-1 (every lane pair: the same value)
         const Fq2<2> t = fq2_fold(fq2_add(inv_get(kU2), inv_xi(fq2_fold(fq2_add(inv_get(kU0), inv_get(kU1))))));
-        const Fq2<2> ti = fq2_fold(fq2_inv(t));
+        const Fq2<2> ti = fq2_fold(fq2_inv<true>(t));  // group 0's four quads hold the same t
         w_sync();
         if (P == 0) inv_put(kTi, ti);
         w_sync();

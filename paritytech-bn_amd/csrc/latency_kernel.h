@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
         const size_t pi = valid ? base + j : n - 1;  // idle slots repeat a real pair
         const int k = pw_slot();
         const bool st = k == 0;
-        const PairAffine a = pair_to_affine(p, q, pi, pi * kL + c, nullptr, err, valid ? mode : 0);
+        const PairAffine a = pair_to_affine<true>(p, q, pi, pi * kL + c, nullptr, err, valid ? mode : 0);
         LAT_STAMP(threadIdx.x == 0, 1);  // producer: to_affine done
         if (st && c == 0) g_lat_skip[j] = a.skip ? 1u : 0u;
         bool dead = false;  // a wait of this wave ran out of its cap

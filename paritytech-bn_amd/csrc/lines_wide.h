@@ -20,6 +20,9 @@ struct PairAffine {
     G2Aff<kPt> qa;
     bool skip;  // a zero point: pairing() of the pair is Fq12::one()
 };
+// Quad: the four lanes of every quad work on the same pair (the eight-lane layouts):
+// the inversion splits its updates over them (tower.h fq_inv_quad)
+template <bool Quad = false>
 __device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t i,
                                                      size_t l, uint8_t* __restrict__ flags, int* __restrict__ err,
                                                      int mode) {
@@ -64,7 +67,7 @@ __device__ __forceinline__ PairAffine pair_to_affine(const bn_g1* __restrict__ p
     if (BN_ALL(p_one && q_one))  // wave-uniform
         t = widen<2>(fq_one());
     else
-        t = fq_inv(fq_mul(pz, nq));
+        t = fq_inv<Quad>(fq_mul(pz, nq));
     const auto pzinv = fq_mul(t, nq);
     const auto ninv = fq_mul(t, pz);
     auto pzinv2 = fq_sqr(pzinv);

@@ -163,11 +163,127 @@ BN_INLINE Fq<2> fq_inv_bgcd(const Fq<B>& x) {
 #endif
     return fq_mul(v, fq_from_limbs<1>(kR3));
 }
-// the inverse is unique, so this equals the reference's binary extended Euclid
-// (arith.rs:324-370 + fp.rs:108-117) bit for bit
+// ---------------------------------------------------------------- the same inversion on a quad of lanes
+// Where the four lanes 4q .. 4q+3 hold the same x (the eight lanes of a pair in
+// k_prepare_wide and the latency kernel's producer, the lane pairs of a wide group)
+// they split each round's four linear updates instead of each running all four:
+// lane 4q + r keeps a (r = 0), b (1), u (2) or v (3) and updates it from its own
+// value and its partner's (quad_perm [1,0,3,2]: a <-> b, u <-> v); the 29 steps on
+// the approximations run on every lane alike, the approximations taken from lanes
+// 0 and 1 of the quad.  One code path for the four updates: (x c + y d + K p) / 2^29
+// with K = 0 on the exact lanes and K = k + 3 * 2^29 on the Montgomery lanes (k
+// clears the low digit; 3 * 2^29 p adds the 3p that keeps the digits non-negative,
+// as bgcd_lin_mont).  The exact update's sign fix (a negative result is negated,
+// and fq_inv_bgcd negates f, g for the (u, v) update with it) reaches the
+// Montgomery lanes as 6p - r, a negation mod p of their result: the same residue.
+// About 0.7x fq_inv_bgcd's instructions per lane; the inverse is unique, so the
+// value is fq_inv_bgcd's (host builds run fq_inv_bgcd itself).
+template <int CTRL>
+BN_INLINE uint32_t quad_perm(uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+#else
+    return v;
+#endif
+}
 template <int B>
+BN_INLINE Fq<2> fq_inv_quad(const Fq<B>& x) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    return fq_inv_bgcd(x);
+#else
+    const uint32_t role = __builtin_amdgcn_workitem_id_x() & 3u;  // 0 a, 1 b, 2 u, 3 v
+    const bool odd = (role & 1u) != 0;
+    const uint32_t mont = role >= 2 ? ~0u : 0u;
+    constexpr Limbs9 P6 = kp_plain(6);
+    const Fq<1> y = fq_canonical(x);
+    uint32_t own[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) own[i] = role == 0 ? y.v[i] : role == 1 ? kP29.v[i] : (role == 2 && i == 0) ? 1u : 0u;
+#pragma unroll 1
+    for (int round = 0; round < kInvRounds; ++round) {
+        // n = max(len(a), len(b), 60) on lanes 0 and 1 (the other lanes' n is unused)
+        uint32_t len = 0;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) len = own[d] != 0 ? 29u * d + 32u - (uint32_t)__builtin_clz(own[d] | 1u) : len;
+        // (the partner's length read once, outside any select: a DPP read placed in a
+        // divergent arm would see the masked-off lanes' stale registers)
+        const uint32_t len_p = quad_perm<0xB1>(len);
+        len = len > len_p ? len : len_p;
+        const uint32_t n = len > 60u ? len : 60u;
+        const uint32_t s = n - 31, dd = s / 29, off = s - 29 * dd;
+        uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+        for (int d = 1; d < 9; ++d) {
+            const bool h = dd == (uint32_t)d;
+            w0 = h ? own[d] : w0;
+            w1 = h ? (d + 1 < 9 ? own[d + 1 < 9 ? d + 1 : 8] : 0u) : w1;
+            w2 = h ? (d + 2 < 9 ? own[d + 2 < 9 ? d + 2 : 8] : 0u) : w2;
+        }
+        const uint64_t wv = (uint64_t)w0 | ((uint64_t)w1 << 29) | ((uint64_t)w2 << 58);
+        const uint64_t ap = (uint64_t)own[0] | (((wv >> off) & 0x7fffffffu) << 29);
+        const uint32_t ap_lo = (uint32_t)ap, ap_hi = (uint32_t)(ap >> 32);
+        uint64_t ab = (uint64_t)quad_perm<0x00>(ap_lo) | ((uint64_t)quad_perm<0x00>(ap_hi) << 32);  // lane 0's a
+        uint64_t bb = (uint64_t)quad_perm<0x55>(ap_lo) | ((uint64_t)quad_perm<0x55>(ap_hi) << 32);  // lane 1's b
+        uint64_t pa = 1, pb = (uint64_t)1 << 32;
+#pragma unroll
+        for (int j = 0; j < 29; ++j) {
+            const bool odd_a = (ab & 1u) != 0;
+            const bool sw = odd_a & (ab < bb);
+            const uint64_t ta = sw ? bb : ab, tb = sw ? ab : bb, tp = sw ? pb : pa, tq = sw ? pa : pb;
+            ab = (ta - (odd_a ? tb : 0)) >> 1;
+            pa = tp - (odd_a ? tq : 0);
+            bb = tb;
+            pb = tq << 1;
+        }
+        const int32_t f0 = (int32_t)(uint32_t)pa, f1 = (int32_t)(uint32_t)pb;
+        const int32_t g0 = (int32_t)((int64_t)(pa - (uint64_t)(int64_t)f0) >> 32);
+        const int32_t g1 = (int32_t)((int64_t)(pb - (uint64_t)(int64_t)f1) >> 32);
+        // a' = a f0 + b g0, b' = a f1 + b g1 (u', v' alike): own * c + partner * e
+        const int32_t c = odd ? g1 : f0, e = odd ? f1 : g0;
+        int64_t t[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+            t[i] = (int64_t)(int32_t)own[i] * c + (int64_t)(int32_t)quad_perm<0xB1>(own[i]) * e;
+        const uint32_t K = ((((uint32_t)t[0] * BN_PINV29) & M29) + (3u << 29)) & mont;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) t[i] += (int64_t)((uint64_t)K * kP29.v[i]);
+        uint32_t r[9];
+        int64_t cr = t[0] >> 29;
+#pragma unroll
+        for (int i = 1; i < 9; ++i) {
+            const int64_t sm = t[i] + cr;
+            r[i - 1] = (uint32_t)sm & M29;
+            cr = sm >> 29;
+        }
+        r[8] = (uint32_t)cr;  // signed top digit on the exact lanes
+        // the exact lanes' sign (lanes 0, 1), also on the Montgomery lanes (quad_perm [0,1,0,1])
+        const uint32_t m = quad_perm<0x44>((uint32_t)((int32_t)r[8] >> 31));
+        Fq<6> z;
+        int64_t cn = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int64_t v = (int64_t)(int32_t)((r[i] ^ m) - m) + (int64_t)(P6.v[i] & m & mont) + cn;
+            z.v[i] = (uint32_t)v & M29;
+            cn = v >> 29;
+        }
+        z.v[8] = (uint32_t)((int64_t)(int32_t)((r[8] ^ m) - m) + (int64_t)(P6.v[8] & m & mont) + cn);
+        // the Montgomery lanes' value (< 6p) back below 2p; a, b <= p stay as they are (q = 0)
+        const Fq<2> zf = fq_fold(z);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) own[i] = zf.v[i];
+    }
+    Fq<2> v;  // lane 3's v
+#pragma unroll
+    for (int i = 0; i < 9; ++i) v.v[i] = quad_perm<0xFF>(own[i]);
+    return fq_mul(v, fq_from_limbs<1>(kR3));
+#endif
+}
+// the inverse is unique, so this equals the reference's binary extended Euclid
+// (arith.rs:324-370 + fp.rs:108-117) bit for bit; Quad: the four lanes of every
+// quad hold the same a (fq_inv_quad)
+template <bool Quad = false, int B>
 BN_INLINE Fq<2> fq_inv(const Fq<B>& a) {
-    return fq_inv_bgcd(a);
+    if constexpr (Quad) return fq_inv_quad(a); else return fq_inv_bgcd(a);
 }
 // x unchanged when its bound is <= L, else folded to 2 (decided at compile time)
 template <int L, int B>
