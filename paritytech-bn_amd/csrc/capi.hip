@@ -642,7 +642,17 @@ uint32_t* parts_region(bn_ctx* c, size_t nchunks) {
 static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out, hipStream_t s) {
     const char* env = getenv("BN254MI_HORNER_TREE");
     const int tree = env ? atoi(env) : 2;  // 2: k_horner_tree2 (default), 1: k_horner_tree, 0: k_horner_wide
-    if (tree == 2 && BN_FE_DUO && plan.S <= kMaxSeg) {
+    static const bool fused = [] {  // $BN254MI_TAIL_FUSED=0: k_seg_fe1 + k_horner_tree2 (A/B)
+        const char* e = getenv("BN254MI_TAIL_FUSED");
+        return !(e && atoi(e) == 0);
+    }();
+    if (tree == 2 && BN_FE_DUO && BN_TAIL_DS && BN_SEG_FE1 && BN_TAIL_M && fused && do_fe && plan.S >= 1 &&
+        plan.S <= kMaxSeg) {
+        // pairing_batch: the whole tail in one launch (kernels_tail.hip k_seg_tail)
+        c->tail_epoch = c->tail_epoch + 1 < (1u << 29) ? c->tail_epoch + 1 : 1u;  // (epoch * 8 fits the role word)
+        k_seg_tail<<<plan.S > 3 ? plan.S : 3, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, d_out, c->d_err,
+                                                                  c->tail_ws, c->tail_epoch);
+    } else if (tree == 2 && BN_FE_DUO && plan.S <= kMaxSeg) {
         // pairing_batch: the segments' first chunks and squarings one block each
         // (k_seg_fe1), the zero flags and the squarer <-> multiplier channel of
         // k_horner_tree2's two blocks at the start of the reduction's ping-pong region
@@ -894,6 +904,7 @@ int bn_ctx_create(int device, bn_ctx** out) {
         hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess ||
+        hipMalloc(&c->tail_ws, kTailWsWords * 4) != hipSuccess || hipMemset(c->tail_ws, 0, kTailWsWords * 4) != hipSuccess ||
         hipMalloc(&c->d_prog, P.s.size() * 4) != hipSuccess ||
         hipMemcpy(c->d_prog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         ctx_teardown(c);  // releases whatever was created (null handles are skipped)
@@ -927,7 +938,7 @@ static void ctx_teardown(bn_ctx* c) {
     for (hipStream_t s : {c->h2d, c->d2h})
         if (s) (void)hipStreamDestroy(s);
     for (void* p : {(void*)c->coeffs, (void*)c->paff, (void*)c->slots, (void*)c->flags, (void*)c->d_err,
-                    (void*)c->d_prog, c->stage})
+                    (void*)c->d_prog, c->stage, (void*)c->tail_ws})
         if (p) (void)hipFree(p);
     for (auto& ev : c->ev_marks)
         for (auto e : ev) c->ev_pool.push_back(e);

@@ -48,6 +48,11 @@ struct bn_ctx {
     // batches of at most this many pairs take k_prepare_wide (8 lanes per pair)
     size_t prepare_wide_max = 0;
     int* d_err = nullptr;
+    // pairing_batch's one-launch tail (kernels_tail.hip k_seg_tail): its own words
+    // (kTailWsWords, zeroed at creation), every word it polls stamped with the
+    // launch's epoch, so no clearing between products
+    uint32_t* tail_ws = nullptr;
+    uint32_t tail_epoch = 0;
     // staging for host-buffer calls (device)
     size_t stage_bytes = 0;
     void* stage = nullptr;

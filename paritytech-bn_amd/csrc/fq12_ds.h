@@ -579,13 +579,14 @@ struct DsChan {
     uint64_t* w;  // (kDsItems + kDsResults) x 128 stamped words of global memory
     int* err;
     uint32_t items, results;
-    bool dead;  // wave-uniform: a take of this wave has run out of its cap
+    bool dead;       // wave-uniform: a take of this wave has run out of its cap
+    uint32_t epoch;  // the stamp: a word is there when its high half equals it (never 0)
 };
-__device__ __forceinline__ void ds_chan_st(uint64_t* slot, uint32_t a) {
+__device__ __forceinline__ void ds_chan_st(uint64_t* slot, uint32_t a, uint32_t epoch) {
     const DsLane x = ds_lane();
     typedef __attribute__((address_space(1))) uint64_t g64;  // global: global_ (not flat) instructions
     if (x.dl && !BN_DS_DROP_STAMPS)
-        __hip_atomic_store((g64*)(slot + 10 * x.cid + x.k), (1ull << 32) | a, __ATOMIC_RELAXED,
+        __hip_atomic_store((g64*)(slot + 10 * x.cid + x.k), ((uint64_t)epoch << 32) | a, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 // every lane of the wave takes part (the spin condition is a wave-wide vote, so
@@ -594,26 +595,26 @@ __device__ __forceinline__ uint32_t ds_chan_ld(const uint64_t* slot, DsChan& ch)
     const DsLane x = ds_lane();
     typedef const __attribute__((address_space(1))) uint64_t g64;
     g64* p = (g64*)(slot + 10 * x.cid + (x.dl ? x.k : 0));
-    uint64_t v = x.dl ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (1ull << 32);
+    uint64_t v = x.dl ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ((uint64_t)ch.epoch << 32);
     if (!ch.dead)
-        for (uint32_t spins = 0; __any((v >> 32) == 0) && spins < kSpinCap; ++spins) {
+        for (uint32_t spins = 0; __any((uint32_t)(v >> 32) != ch.epoch) && spins < kSpinCap; ++spins) {
             __builtin_amdgcn_s_sleep(1);
             if (x.dl) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-    if (__any((v >> 32) == 0)) {  // decided on the words themselves: one that arrived during the last sleep counts
+    if (__any((uint32_t)(v >> 32) != ch.epoch)) {  // decided on the words themselves: one that arrived during the last sleep counts
         if (!ch.dead && ch.err && (threadIdx.x & 63u) == 0) err_or(ch.err, BN_ERR_INTERNAL);
         ch.dead = true;
     }
     return x.dl ? (uint32_t)v : 0u;
 }
 __device__ __forceinline__ void ds_put(DsChan& ch, uint32_t a) {  // S
-    ds_chan_st(ch.w + 128 * (ch.items++), a);
+    ds_chan_st(ch.w + 128 * (ch.items++), a, ch.epoch);
 }
 __device__ __forceinline__ uint32_t ds_take(DsChan& ch) {  // M
     return ds_chan_ld(ch.w + 128 * (ch.items++), ch);
 }
 __device__ __forceinline__ void ds_put_result(DsChan& ch, uint32_t a) {  // M
-    ds_chan_st(ch.w + 128 * (kDsItems + ch.results++), a);
+    ds_chan_st(ch.w + 128 * (kDsItems + ch.results++), a, ch.epoch);
 }
 __device__ __forceinline__ uint32_t ds_get_result(DsChan& ch) {  // S
     return ds_chan_ld(ch.w + 128 * (kDsItems + ch.results++), ch);
@@ -701,6 +702,90 @@ __device__ __forceinline__ void ds_fe_last_m(DsChan& ch) {
     ds_put_result(ch, ds_frob<1>(l));   // o
     const uint32_t t = ds_mul(l, s, true);  // conj(s) * l
     ds_put_result(ch, ds_frob<3>(t));   // u
+}
+
+// ---------------------------------------------------------------- two multiplier blocks
+// One multiplier falls behind the squarer: its 23 products per exponentiation (~3 us
+// each) take longer than S's 62 squarings (~0.93 us), so S waited ~15 us for each
+// exponentiation's result (tools/tail_stamps.py, profiles/r6i_tail_stamps.json).  With
+// two, M_0 multiplies the even and M_1 the odd hand-overs of each exponentiation (the
+// same slots: item numbers as ds_fe_last_s), each returns its partial product
+// conjugated, and S multiplies the two (conj is multiplicative and the product
+// commutes: the value of ds_exp_sq).  Results: exponentiation e's partials in slots
+// 2e and 2e + 1, then o and u (M_0) in 6 and 7.
+static_assert(kDsResults >= 8, "three pairs of partials, o and u");
+__device__ __forceinline__ uint32_t ds_exp_sq2(uint32_t xx, DsChan& ch, int stamp = -1) {
+#pragma unroll 1
+    for (int k = 0;; ++k) {
+        if ((kZNaf.nz >> k) & 1u) ds_put(ch, xx);
+        if (k == kZNaf.top) break;
+        xx = ds_cyc_body(xx);
+    }
+    if (BN_TAIL_STAMPS && stamp >= 0) TAIL_STAMP(stamp);
+    const uint32_t r0 = ds_get_result(ch);
+    const uint32_t r1 = ds_get_result(ch);
+    return ds_mul(r0, r1, false);
+}
+// M_par's share of exponentiation e (its hand-overs from item ch.items on); returns
+// the first hand-over (x itself) on M_0
+__device__ __forceinline__ uint32_t ds_exp_mul2(DsChan& ch, int par, int e) {
+    uint32_t acc = 0, x0 = 0;
+    int j = 0;
+#pragma unroll 1
+    for (int k = 0; k <= kZNaf.top; ++k) {
+        if (!((kZNaf.nz >> k) & 1u)) continue;
+        if ((j & 1) == par) {
+            const uint32_t y = ds_chan_ld(ch.w + 128 * (ch.items + j), ch);
+            const bool cj = ((kZNaf.minus >> k) & 1u) != 0;
+            if (j == par) {
+                x0 = y;
+                acc = cj ? ds_conj(y) : y;
+            } else {
+                acc = ds_mul(acc, y, cj);
+            }
+        }
+        ++j;
+    }
+    ch.items += j;
+    ds_chan_st(ch.w + 128 * (kDsItems + 2 * e + par), ds_conj(acc), ch.epoch);
+    return x0;
+}
+__device__ __forceinline__ uint32_t ds_fe_last_s2(uint32_t s, DsChan& ch) {
+    const uint32_t a = ds_exp_sq2(s, ch, 2);
+    TAIL_STAMP(3);
+    const uint32_t b = ds_cyc(a);
+    ds_put(ch, b);
+    const uint32_t c = ds_cyc(b);
+    const uint32_t d = ds_mul(c, b, false);
+    const uint32_t e = ds_exp_sq2(d, ch, 4);
+    TAIL_STAMP(5);
+    const uint32_t f1 = ds_cyc(e);
+    const uint32_t g = ds_exp_sq2(f1, ch, 6);
+    TAIL_STAMP(7);
+    const uint32_t j = ds_mul(e, g, true);  // conj(g) * e
+    const uint32_t k = ds_mul(j, d, true);  // j * conj(d)
+    ds_put(ch, k);
+    const uint32_t m = ds_mul(k, e, false);
+    const uint32_t n = ds_mul(s, m, false);
+    const uint32_t q = ds_frob<2>(k);
+    const uint32_t o = ds_get_result(ch);
+    const uint32_t p = ds_mul(o, n, false);
+    const uint32_t r = ds_mul(q, p, false);
+    const uint32_t u = ds_get_result(ch);
+    return ds_mul(u, r, false);
+}
+__device__ __forceinline__ void ds_fe_last_m2(DsChan& ch, int par) {
+    const uint32_t s = ds_exp_mul2(ch, par, 0);  // a's partial; s on M_0
+    uint32_t b = 0;
+    if (par == 0) b = ds_take(ch); else ++ch.items;
+    (void)ds_exp_mul2(ch, par, 1);              // e
+    (void)ds_exp_mul2(ch, par, 2);              // g
+    if (par != 0) return;
+    const uint32_t k = ds_take(ch);
+    const uint32_t l = ds_mul(k, b, false);
+    ds_chan_st(ch.w + 128 * (kDsItems + 6), ds_frob<1>(l), ch.epoch);     // o
+    const uint32_t t = ds_mul(l, s, true);                                  // conj(s) * l
+    ds_chan_st(ch.w + 128 * (kDsItems + 7), ds_frob<3>(t), ch.epoch);     // u
 }
 
 }  // namespace bn

@@ -589,6 +589,14 @@ constexpr int kTailChanWords = 1024 + 2 * 128 * 88;
 // blocks (the final exponentiation's squarer and multiplier)
 __global__ void __launch_bounds__(kTailBlock) k_seg_fe1(uint32_t* __restrict__ g, SegPlan plan,
                                                         uint32_t* __restrict__ zf);
+// pairing_batch's whole tail in one launch of max(S, 3) blocks (k_seg_fe1, the
+// segments' product as a chain of nodes completed by whichever block arrives second,
+// the last chunk on the squarer and two multipliers): ws = bn_ctx.tail_ws, every word
+// it polls stamped with `epoch` (1 .. 2^29 - 1, a new one per launch)
+constexpr int kTailWsWords = kTailChanWords + 2 * kMaxSeg * 256;
+__global__ void __launch_bounds__(kTailBlock) k_seg_tail(const uint32_t* __restrict__ g, SegPlan plan,
+                                                         bn_gt* __restrict__ out, int* __restrict__ err,
+                                                         uint32_t* __restrict__ ws, uint32_t epoch);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
 // (a producer wave for the lines, consumer groups for the wide Miller loop + FE)
 constexpr int kLatPairs = 8;

@@ -239,6 +239,153 @@ __global__ void __launch_bounds__(kTailThreads) k_seg_fe1(uint32_t* __restrict__
     if (threadIdx.x < 12) w_st_split(g, (size_t)plan.S, (size_t)s, w, x);
     if (BN_TAIL_STAMPS && s == 0) TAIL_STAMP(18);
 }
+
+// ---------------------------------------------------------------- the whole tail in one launch
+// pairing_batch's tail as ONE launch of max(S, 3) blocks, without k_horner_tree2's
+// launch and its 16-lane product tree (four levels of w12_mul, ~21 us): block s < S
+// runs segment s's first chunk and squarings as k_seg_fe1 does, then the segment
+// values meet in a chain of nodes.  Node k joins d_k (block k, side 0) with
+// P_(k+1) = d_(k+1) ... d_(S-1) (side 1: its carrier; block S - 1 carries d_(S-1) to
+// node S - 2): both sides store their value (stamped words) and swap the node's word
+// to the epoch; the one that finds the epoch there is second, reads the other side's
+// value, multiplies, and carries P_k on to node k - 1; the first one is done.
+// e_s falls with s, so the blocks arrive in the order S - 1, ..., 0 and P_1 is
+// (mostly) ready when block 0 gets there: the product costs one digit-sliced product
+// behind the longest segment.  No block waits for one that may not have started: the
+// second arriver reads a value whose writer has already arrived.  A block that leaves
+// a node first (and the spare blocks of a plan with S < 3) offers itself as one of
+// the last chunk's two multipliers (fq12_ds.h ds_fe_last_m2); the carrier of P_0
+// runs the last chunk as the squarer, with both multipliers if two have claimed the
+// role by then, else alone.  Roles are claimed on an epoch-tagged word, never
+// assumed (as k_horner_tree2's): bit 0 / 1 = M_0 / M_1 claimed, bit 2 = the squarer
+// has decided; a multiplier waits for that decision and leaves unless it is two.  A zero segment value makes the product zero, and
+// the final exponentiation of zero is zero: the carrier tests its result (the
+// reference's None, fq12.rs:63-72).  Values are the same as k_seg_fe1 + k_horner_tree2
+// (Fq12 products commute).
+constexpr int kLinkNodeOff = kRoleWord + 1;     // node k's word
+constexpr int kLinkOff = kDsChanOff + kDsChanWords;  // node k side j: 128 stamped words at slot 2k + j
+static_assert(kLinkNodeOff + kMaxSeg <= kDsChanOff && kLinkOff + 2 * kMaxSeg * 256 <= kTailWsWords, "tail words");
+// the role word: epoch * 8 + bits (bit 0: M_0 claimed, bit 1: M_1, bit 2: the squarer decided)
+constexpr uint32_t kTailM0 = 1, kTailM1 = 2, kTailDecided = 4;
+typedef __attribute__((address_space(1))) uint32_t tail_word;
+__device__ __forceinline__ uint32_t tail_bits(uint32_t cur, uint32_t epoch) { return (cur >> 3) == epoch ? cur & 7u : 0u; }
+// thread 0 of a multiplier candidate: 1 + par when it got M_par, 0 when none is left
+__device__ uint32_t tail_claim_m(uint32_t* rw, uint32_t epoch) {
+    tail_word* p = (tail_word*)rw;
+    uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        const uint32_t b = tail_bits(cur, epoch);
+        if (b & kTailDecided) return 0;
+        const uint32_t add = !(b & kTailM0) ? kTailM0 : !(b & kTailM1) ? kTailM1 : 0u;
+        if (!add) return 0;
+        if (__hip_atomic_compare_exchange_strong(p, &cur, epoch * 8u + (b | add), __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return add == kTailM0 ? 1u : 2u;
+    }
+}
+// thread 0 of the squarer: sets the decided bit; returns the multiplier bits at that moment
+__device__ uint32_t tail_decide(uint32_t* rw, uint32_t epoch) {
+    tail_word* p = (tail_word*)rw;
+    uint32_t cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        const uint32_t b = tail_bits(cur, epoch);
+        if (__hip_atomic_compare_exchange_strong(p, &cur, epoch * 8u + (b | kTailDecided), __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            return b & (kTailM0 | kTailM1);
+    }
+}
+// thread 0 of a multiplier: the squarer's decision (its multiplier bits), or 0 when the
+// wait runs out of its cap (the call fails: BN_ERR_INTERNAL)
+__device__ uint32_t tail_await_decision(uint32_t* rw, uint32_t epoch, int* err) {
+    tail_word* p = (tail_word*)rw;
+    for (uint32_t spins = 0; spins < kSpinCap; ++spins) {
+        const uint32_t b = tail_bits(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), epoch);
+        if (b & kTailDecided) return b & (kTailM0 | kTailM1);
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (err) err_or(err, BN_ERR_INTERNAL);
+    return 0;
+}
+__global__ void __launch_bounds__(kTailThreads) k_seg_tail(const uint32_t* __restrict__ g, SegPlan plan,
+                                                           bn_gt* __restrict__ out, int* __restrict__ err,
+                                                           uint32_t* __restrict__ ws, uint32_t epoch) {
+    fold_table_init();
+    const WL w = wl();
+    const int s = (int)blockIdx.x;
+    uint64_t* const link = (uint64_t*)(ws + kLinkOff);
+    DsChan ch = {(uint64_t*)(ws + kDsChanOff), err, 0, 0, false, epoch};  // its dead flag serves the chain too
+    bool carrier = false;
+    uint32_t d = 0;
+    if (s < plan.S) {
+        int e = 0;
+        for (int t = s + 1; t < plan.S; ++t) e += plan.hi[t] - plan.lo[t];
+        Fq<2> x = widen<2>(fq_zero());
+        if (threadIdx.x < (unsigned)kWLanes) x = w_ld_split(g, (size_t)plan.S, (size_t)s, w);  // group 0
+        if (BN_TAIL_STAMPS && s == 0) TAIL_STAMP(16);
+        x = w12_fe_first_par(x);
+        if (BN_TAIL_STAMPS && s == 0) TAIL_STAMP(17);
+        ds_init();
+        d = ds_from_w12(x);
+#pragma unroll 1
+        for (int k = 0; k < e; ++k) d = ds_cyc_body(d);
+        if (BN_TAIL_STAMPS && s == 0) TAIL_STAMP(18);
+        carrier = true;
+        int k = s == plan.S - 1 ? s - 1 : s, side = s == plan.S - 1 ? 1 : 0;
+#pragma unroll 1
+        for (; k >= 0; --k, side = 1) {
+            ds_chan_st(link + 128 * (2 * k + side), d, epoch);
+            __syncthreads();  // every digit lane's store is issued before the arrival
+            if (threadIdx.x == 0)
+                g_tail_role = __hip_atomic_exchange((__attribute__((address_space(1))) uint32_t*)(ws + kLinkNodeOff + k),
+                                                    epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (g_tail_role != epoch) {  // first at node k: the other side carries on
+                carrier = false;
+                break;
+            }
+            d = ds_mul(d, ds_chan_ld(link + 128 * (2 * k + 1 - side), ch), false);
+        }
+    } else {
+        ds_init();
+    }
+    if (!carrier) {  // one of the last chunk's multipliers, if a role is still free
+#if BN_TAIL_LATE_M
+        for (int t = 0; t < 40000; ++t) __builtin_amdgcn_s_sleep(1);
+#endif
+        __syncthreads();
+        if (threadIdx.x == 0) g_tail_role = tail_claim_m(ws + kRoleWord, epoch);
+        __syncthreads();
+        const uint32_t role = g_tail_role;
+        if (role == 0) return;
+        __syncthreads();
+        if (threadIdx.x == 0) g_tail_role = tail_await_decision(ws + kRoleWord, epoch, err);
+        __syncthreads();
+        if (g_tail_role != (kTailM0 | kTailM1)) return;  // the squarer went on alone
+        if (BN_TAIL_STAMPS) TAIL_STAMP(role == 1 ? 25 : 27);
+        ds_fe_last_m2(ch, (int)role - 1);
+        if (BN_TAIL_STAMPS) TAIL_STAMP(role == 1 ? 26 : 28);
+        return;
+    }
+    // the carrier of P_0: the squarer
+    if (BN_TAIL_STAMPS) TAIL_STAMP(1);
+    __syncthreads();
+    if (threadIdx.x == 0) g_tail_role = tail_decide(ws + kRoleWord, epoch);
+    __syncthreads();
+    if (g_tail_role == (kTailM0 | kTailM1))
+        d = ds_fe_last_s2(d, ch);
+    else
+        d = ds_fe_last(d);
+    if (BN_TAIL_STAMPS) TAIL_STAMP(8);
+    const Fq<2> r = ds_to_w12(d);  // threads 0..11 get the value
+    const bool z = w12_is_zero(r);
+    if (threadIdx.x == 0) g_tail_zero = z ? 1u : 0u;
+    __syncthreads();
+    const bool zero = g_tail_zero != 0;
+    if (zero && err && threadIdx.x == 0) err_or(err, BN_ERR_FE_ZERO);
+    uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!zero && threadIdx.x < 12) fq_store_ref(r, words);
+    if (threadIdx.x < 12) st_words(&out[0].c[w_gt_index(w)], words);
+}
 #endif
 
 // g: the S segment values (element s of a split-layout array of stride S);
@@ -276,7 +423,7 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
         if (g_tail_role != 0) return;  // the squarer block has gone on alone
         if (BN_TAIL_STAMPS) TAIL_STAMP(25);
         ds_init();
-        DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0, false};
+        DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0, false, 1};
         ds_fe_last_m(ch);
         if (BN_TAIL_STAMPS) TAIL_STAMP(26);
         return;
@@ -335,7 +482,7 @@ __global__ void __launch_bounds__(kTailThreads) k_horner_tree2(const uint32_t* _
             duo = g_tail_role == kRoleM;
         }
         if (duo) {
-            DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0, false};
+            DsChan ch = {(uint64_t*)(const_cast<uint32_t*>(zf) + kDsChanOff), err, 0, 0, false, 1};
             d = ds_fe_last_s(d, ch);
         } else {
             d = ds_fe_last(d);

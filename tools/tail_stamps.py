@@ -4,7 +4,8 @@
 bn_pairing_batch_dev products, then the s_memrealtime (100 MHz) stamps thread 0 of a
 block wrote (fq12_ds.h TAIL_STAMP), in us from k_seg_fe1's start:
   k_seg_fe1, segment 0's block: start, first chunk done (the Fq12 inversion), squarings done;
-  k_horner_tree2's squarer block S: start, tree done, then per exp_by_neg_z the end of its
+  k_horner_tree2's squarer block S: start, tree done (k_seg_tail, BN254MI_TAIL_FUSED=1: no
+  start stamp; "tree done" is the carrier of the segments' product starting the last chunk), then per exp_by_neg_z the end of its
   squarings and the arrival of M's product, and the last chunk done;
   its multiplier block M: start, role claimed, done.
 Prints the median of the five per stamp as one JSON line."""
@@ -19,9 +20,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "paritytech-bn_amd"))
 sys.path.insert(0, ROOT)
 NAMES = {16: "fe1_start", 17: "fe1_first_chunk_done", 18: "fe1_squarings_done",
-         0: "S_start", 1: "S_tree_done", 2: "S_exp1_squarings_done", 3: "S_exp1_result_in",
+         0: "S_start", 1: "S_tree_done (k_seg_tail: the chain's product in)", 2: "S_exp1_squarings_done", 3: "S_exp1_result_in",
          4: "S_exp2_squarings_done", 5: "S_exp2_result_in", 6: "S_exp3_squarings_done", 7: "S_exp3_result_in",
-         8: "S_last_chunk_done", 24: "M_start", 25: "M_claimed", 26: "M_done"}
+         8: "S_last_chunk_done", 24: "M_start", 25: "M_claimed", 26: "M_done",
+         27: "M1_claimed (k_seg_tail)", 28: "M1_done (k_seg_tail)"}
 
 
 def main():
