@@ -34,7 +34,9 @@ def code_of(fn):
 def tail_probe(kind):
     """libbn254mi_chanfail.so / libbn254mi_latem.so: only the product's tail differs
     from the product build (paritytech-bn_amd/Makefile), so only the segmented
-    pairing_batch (4,224 terms: k_seg_fe1 + k_horner_tree2 on two blocks) is run."""
+    pairing_batch (4,224 terms) is run: its tail is k_seg_tail (one launch, the
+    segment chain and two multiplier blocks), or k_seg_fe1 + k_horner_tree2 with
+    BN254MI_TAIL_FUSED=0.  kind "main": the product library itself (FAILURE_PROBE_TAIL=1)."""
     ctx = _native.Context(0)
     p, q, _, _ = O.random_pairs(24, seed=43, nthreads=8)
     reps = 4224 // 24
@@ -55,6 +57,8 @@ def main():
     for kind in ("chanfail", "latem"):
         if _native.LIB_PATH.endswith("libbn254mi_%s.so" % kind):
             return tail_probe(kind)
+    if os.environ.get("FAILURE_PROBE_TAIL") == "1":
+        return tail_probe("main")
     assert _native.LIB_PATH.endswith("libbn254mi_cap0.so"), _native.LIB_PATH
     ctx = _native.Context(0)
     n = 24

@@ -56,10 +56,10 @@ def test_capped_handoff_fails_the_call():
     assert res["throughput_path"] == BN_OK and res["throughput_path_bit_exact"], res
 
 
-def _tail_probe(lib):
+def _tail_probe(lib, fused=1):
     path = os.path.join(ROOT, "paritytech-bn_amd", lib)
     assert os.path.exists(path), "%s not built: make -C paritytech-bn_amd chanfail latem" % lib
-    env = dict(os.environ, BN254MI_LIB=path)
+    env = dict(os.environ, BN254MI_LIB=path, BN254MI_TAIL_FUSED=str(fused), FAILURE_PROBE_TAIL="1")
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "tests", "failure_probe.py")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
@@ -67,20 +67,33 @@ def _tail_probe(lib):
 
 
 @pytest.mark.gpu
-def test_tail_channel_fails_fast_after_one_expired_wait():
-    """Every store of the squarer <-> multiplier channel dropped, at a spin cap of 2^20
+@pytest.mark.parametrize("fused", [1, 0])
+def test_tail_channel_fails_fast_after_one_expired_wait(fused):
+    """Every store of the tail's global-memory channel dropped, at a spin cap of 2^20
     polls (~60 ms per expired wait): without the channel's sticky `dead` flag
     (fq12_ds.h ds_chan_ld) the multiplier's 80 takes and the squarer's 5 result
-    reads would each spin out, ~5 s; with it each wave spins out once."""
-    res = _tail_probe("libbn254mi_chanfail.so")
+    reads would each spin out, ~5 s; with it each wave spins out once.  fused = 1:
+    k_seg_tail (the segment chain's reads share the flag), 0: k_seg_fe1 + k_horner_tree2."""
+    res = _tail_probe("libbn254mi_chanfail.so", fused)
     assert res["code"] == BN_ERR_INTERNAL and not res["value_returned"], res
     assert res["seconds_1"] < 1.5, res
 
 
 @pytest.mark.gpu
-def test_tail_squarer_goes_on_alone_when_the_multiplier_is_late():
-    """The multiplier block of k_horner_tree2 starting ~2 ms late (as when other work
-    holds the CUs): the squarer claims the last chunk alone (kernels_tail.hip role
-    word), the late block returns, and the product is bit-exact."""
-    res = _tail_probe("libbn254mi_latem.so")
+@pytest.mark.parametrize("fused", [1, 0])
+def test_tail_squarer_goes_on_alone_when_the_multiplier_is_late(fused):
+    """The multiplier blocks starting ~2 ms late (as when other work holds the CUs):
+    the squarer decides for the last chunk alone (kernels_tail.hip role word), the
+    late blocks return, and the product is bit-exact (fused = 1: k_seg_tail's
+    multiplier candidates; 0: k_horner_tree2's block 1)."""
+    res = _tail_probe("libbn254mi_latem.so", fused)
+    assert res["code"] == BN_OK and res["value_returned"] and res["bit_exact"], res
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fused", [1, 0])
+def test_tail_forms_bit_exact(fused):
+    """The product library's two tails on the 4,224-term segmented pairing_batch:
+    k_seg_tail (default) and k_seg_fe1 + k_horner_tree2 (BN254MI_TAIL_FUSED=0)."""
+    res = _tail_probe("libbn254mi.so", fused)
     assert res["code"] == BN_OK and res["value_returned"] and res["bit_exact"], res
