@@ -262,7 +262,7 @@ def product_affine_inputs(ctx, Pd, Qd, n, stream, dev, args, ref):
 def products_in_flight(ctx, Pd, Qd, n, stream, dev, args, ref):
     """Config 5 as a stream of independent pairing-product checks, two at a time:
     product k runs on context k % 2 (own workspace, own stream), so one product's
-    latency-bound tail (k_seg_fe1 on 16 CUs, k_horner_tree2 on 2) overlaps the next
+    latency-bound tail (k_seg_tail: 16 CUs, then 3) overlaps the next
     product's issue-bound front on the other CUs.  Reported beside the one-product
     latency (`ms_per_step`, the line's value), never as it.  Both contexts' last
     products are checked against the oracle's value of the same inputs."""
@@ -340,9 +340,10 @@ def other_workload(args, local_rank):
         res["config"] = {"workload": "BASELINE config 5: one pairing_batch over 2^14 terms, HBM-resident inputs "
                                      "(bn_pairing_batch_dev: per-term lines (k_prepare_wide), the segmented "
                                      "shared-squaring Miller loop (k_miller_seg), the device product reduction "
-                                     "(k_fq12_reduce_wide, one or two levels), then per segment the final "
-                                     "exponentiation's first chunk and Horner squarings (k_seg_fe1) and the tree + "
-                                     "last chunk digit-sliced on two blocks (k_horner_tree2))", "terms": n}
+                                     "(k_fq12_reduce_wide, one or two levels), then the tail in one launch "
+                                     "(k_seg_tail: per segment the final exponentiation's first chunk and Horner "
+                                     "squarings, the segments' product as a chain, the last chunk digit-sliced on "
+                                     "a squarer and two multiplier blocks)", "terms": n}
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -372,7 +373,7 @@ def other_workload(args, local_rank):
                                              "corrected) + WRITE_SIZE of every kernel of one product, committed "
                                              "rocprofv3 PMC passes, not measured in this run",
                            "kernel": "whole product (k_prepare_wide, k_miller_seg, k_fq12_reduce_wide, "
-                                     "k_seg_fe1, k_horner_tree2)",
+                                     "k_seg_tail)",
                            "per_step_ms": ms,
                            "basis": "SURVEY.md 8(d) config 5: n*(19+2655+3741) + 2304 + 8767 Fq-mul, x128 MAD32"}
         threads = host_cpus()["usable"]

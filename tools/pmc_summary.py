@@ -139,13 +139,14 @@ for k, v in sorted(agg.items()):
                           "WRITE_SIZE as counted (MI355X_MICROARCH §HBM); source %s" % tag}
     lines.append("%-16s %14.3e %14.3e %14.3e %12.3e %10.3f" % (k, fetch, write, valu, cyc, valu / cyc if cyc else 0))
 if prod:
-    # one product step = one launch of the last kernel (k_horner_tree2 since round 5, k_horner_tree
-    # before); its traffic is every launch's bytes in the pass
-    steps = (len(prod.get("k_horner_tree2", {}).get("FETCH_SIZE", []))
+    # one product step = one launch of the last kernel (k_seg_tail since round 6, k_horner_tree2 in
+    # round 5, k_horner_tree before); its traffic is every launch's bytes in the pass
+    steps = (len(prod.get("k_seg_tail", {}).get("FETCH_SIZE", []))
+             or len(prod.get("k_horner_tree2", {}).get("FETCH_SIZE", []))
              or len(prod.get("k_horner_tree", {}).get("FETCH_SIZE", [])) or 1)
     per_kernel = {}
     product_kernels = ("k_prepare_wide", "k_prepare", "k_miller_seg", "k_fq12_reduce_wide", "k_horner_tree",
-                       "k_horner_tree2", "k_seg_fe1", "k_horner_wide", "k_pairing_latency", "k_err_status")  # not the bench's input generation
+                       "k_horner_tree2", "k_seg_fe1", "k_seg_tail", "k_horner_wide", "k_pairing_latency", "k_err_status")  # not the bench's input generation
     for k, v in prod.items():
         if k not in product_kernels:
             continue
