@@ -291,13 +291,14 @@ void par_copy(void* dst, const void* src, size_t bytes) {
 // to_affine + the 87 line coefficients of m pairs into c->coeffs / paff / flags:
 // eight lanes per pair (k_prepare_wide, about a third of the step latency) while
 // the batch leaves the GPU underfilled, two lanes per pair (k_prepare) otherwise
-static int prepare(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int mode, hipStream_t s) {
+// (scale: 1 for the Miller-loop consumers, 0 for the coefficient export)
+static int prepare(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t m, int mode, hipStream_t s, int scale = 1) {
     if (m <= c->prepare_wide_max)
         k_prepare_wide<<<grid_pair(kPrepareWideLanes * m), kPairBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff,
-                                                                              c->flags, c->d_err, mode);
+                                                                              c->flags, c->d_err, mode, scale);
     else
         k_prepare<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(d_p, d_q, m, c->coeffs, c->paff, c->flags, c->d_err,
-                                                                   mode);
+                                                                   mode, scale);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
 }
@@ -1037,7 +1038,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             mark(1);
         } else {
             k_prepare<<<grid_pair(kPathLanes * m), kPairBlock, 0, s>>>(d_p + off, d_q + off, m, c->coeffs, c->paff, c->flags,
-                                                                  c->d_err, 0);
+                                                                  c->d_err, 0, 1);
             mark(1);
             if (c->miller_form == 2) {  // the segment kernel with one segment: the whole loop
                 const SegPlan whole = plan_layout(cut_plan(1, 1), m, 1);  // one segment: the whole loop
@@ -1427,7 +1428,7 @@ int bn_g2_precompute_many(bn_ctx* c, const bn_g2* q, size_t n, bn_fq2* out) {
         std::vector<bn_g1> ones(m, one);
         HIPCHK(c, hipMemcpyAsync(dp, ones.data(), m * sizeof(bn_g1), hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(dq, q + off, m * sizeof(bn_g2), hipMemcpyHostToDevice, c->stream));
-        RET_IF(prepare(c, dp, dq, m, 1, c->stream));
+        RET_IF(prepare(c, dp, dq, m, 1, c->stream, 0));  // the reference's (unscaled) coefficients
         k_coeffs_store<<<grid_for(kPathLanes * m), kBlock, 0, c->stream>>>(c->coeffs, m, dout);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemcpyAsync(out + off * BN_NUM_COEFFS * 3, dout, out_bytes, hipMemcpyDeviceToHost, c->stream));

@@ -545,14 +545,26 @@ __global__ void __launch_bounds__(kBlock) k_horner_tree(const uint32_t* __restri
                                                         bn_gt* __restrict__ out, int* __restrict__ err, int duo);
 __global__ void __launch_bounds__(kPairBlock) k_prepare(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q, size_t n,
                           uint32_t* __restrict__ coeffs, uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
-                          int* __restrict__ err, int mode);
+                          int* __restrict__ err, int mode, int scale);
 // the same outputs on kPrepareWideLanes lanes per pair (kernels_pairing.hip): four
-// lane pairs run each line step's independent products side by side
+// lane pairs run each line step's independent products side by side.  scale = 1: the
+// lines as the Miller loop multiplies by them (ell_vw Py, ell_vv Px; the consumers of
+// coeffs expect that form in a BN_LINES_PRESCALED build), 0: the reference's
+// coefficients (the G2Precomp export)
 constexpr int kPrepareWideLanes = 8;
+// BN_LINES_PRESCALED: the producers store each line as the Miller loop multiplies by it
+// (ell_0, ell_vw * Py, ell_vv * Px; mod.rs:589), so k_miller_seg / k_miller apply it
+// without scaling, and the latency kernel's producer writes it to its ring that way
+// (lines_wide.h PwEll: the eight-lane steps take the two P products in slots their
+// layers left duplicated); `scale` = 0 keeps the reference's G2Precomp coefficients
+// (the bn_g2_precompute export).  0: the consumers scale.
+#ifndef BN_LINES_PRESCALED
+#define BN_LINES_PRESCALED 1
+#endif
 __global__ void __launch_bounds__(kPairBlock) k_prepare_wide(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,
                                                          size_t n, uint32_t* __restrict__ coeffs,
                                                          uint32_t* __restrict__ paff, uint8_t* __restrict__ flags,
-                                                         int* __restrict__ err, int mode);
+                                                         int* __restrict__ err, int mode, int scale);
 __global__ void __launch_bounds__(kBlock) k_coeffs_store(const uint32_t* __restrict__ coeffs, size_t n,
                                                          bn_fq2* __restrict__ out);
 __global__ void __launch_bounds__(kPairBlock) k_pairing_fused(const bn_g1* __restrict__ p, const bn_g2* __restrict__ q,

@@ -22,7 +22,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_prepare(const bn_g1
                                                                     uint32_t* __restrict__ coeffs,
                                                                     uint32_t* __restrict__ paff,
                                                                     uint8_t* __restrict__ flags,
-                                                                    int* __restrict__ err, int mode) {
+                                                                    int* __restrict__ err, int mode, int scale) {
     fold_table_init();
     const Balance bal = balance_init();
     const size_t l = lane_id(), i = l / kL, nl = kL * n;
@@ -30,11 +30,17 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_prepare(const bn_g1
     const PairAffine a = pair_to_affine(p, q, i, l, flags, err, mode);
     st_fq(paff, nl, l, 0, a.px);
     st_fq(paff, nl, l, 1, a.py);
+    const bool sc = BN_LINES_PRESCALED && scale;
     g2_precompute(a.qa, [&](int k, const Ell& e) {
         balance_step(bal, (uint32_t)k);
         st_fq2(coeffs, nl, l, k * 6 + 0, e.ell_0);
-        st_fq2(coeffs, nl, l, k * 6 + 2, e.ell_vw);
-        st_fq2(coeffs, nl, l, k * 6 + 4, e.ell_vv);
+        if (sc) {  // wave-uniform
+            st_fq2(coeffs, nl, l, k * 6 + 2, narrow<kLine>(fq2_scale(e.ell_vw, a.py)));
+            st_fq2(coeffs, nl, l, k * 6 + 4, narrow<kLine>(fq2_scale(e.ell_vv, a.px)));
+        } else {
+            st_fq2(coeffs, nl, l, k * 6 + 2, e.ell_vw);
+            st_fq2(coeffs, nl, l, k * 6 + 4, e.ell_vv);
+        }
     });
 }
 
@@ -45,7 +51,8 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_prepare_wide(const 
                                                                          uint32_t* __restrict__ coeffs,
                                                                          uint32_t* __restrict__ paff,
                                                                          uint8_t* __restrict__ flags,
-                                                                         int* __restrict__ err, int mode) {
+                                                                         int* __restrict__ err, int mode,
+                                                                         int scale) {
     fold_table_init();
     const Balance bal = balance_init();
     const size_t l = lane_id(), i = l / kPW, nl = kL * n;
@@ -58,18 +65,55 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_prepare_wide(const 
         st_fq(paff, nl, lt, 0, a.px);
         st_fq(paff, nl, lt, 1, a.py);
     }
-    auto emit = [&](int c, const Ell& e) {
-        if (st) {
-            st_fq2(coeffs, nl, lt, c * 6 + 0, e.ell_0);
-            st_fq2(coeffs, nl, lt, c * 6 + 2, e.ell_vw);
-            st_fq2(coeffs, nl, lt, c * 6 + 4, e.ell_vv);
-        }
-    };
     // g2_precompute (pairing.h), AffineG2::precompute mod.rs:701-727
     const G2Aff<kPt>& qa = a.qa;
     G2Proj r = {qa.x, qa.y, widen<kPt>(fq2_one())};
     const auto qy_neg = fq2_neg(qa.y);
     int c = 0;
+#if BN_LINES_PRESCALED
+    // slot 0 stores ell_0; with `scale` slot 2 stores ell_vw * Py and slot 3 ell_vv * Px
+    // (their own products, lines_wide.h PwEll), else slot 0 the unscaled pair
+    const bool sc = scale != 0;
+    // (one select and one store per lane, at a per-slot offset: with a store per slot
+    // under its own branch the compiler staged the values through scratch)
+    auto emit = [&](int cc, const PwEll& e) {
+        if (sc) {
+            const Fq2<kLine> x = fq2_select(k == 0, e.e.ell_0, fq2_select(k == 2, e.vw_py, e.vv_px));
+            if (k != 1) st_fq2(coeffs, nl, lt, cc * 6 + (k == 0 ? 0 : k == 2 ? 2 : 4), x);
+        } else if (st) {
+            st_fq2(coeffs, nl, lt, cc * 6 + 0, e.e.ell_0);
+            st_fq2(coeffs, nl, lt, cc * 6 + 2, e.e.ell_vw);
+            st_fq2(coeffs, nl, lt, cc * 6 + 4, e.e.ell_vv);
+        }
+    };
+    const Fq2<2> py_r = pw_real(a.py);
+    const Fq2<2> px_r = pw_real(a.px);
+    const auto px3_r = pw_real(fq_add(fq_add(a.px, a.px), a.px));
+    const auto bxpy_q = fq2_scale(qa.x, a.py);  // base x * Py of Q (and -Q)
+#pragma unroll 1
+    for (int d = 0; d < BN_NAF_DIGITS; ++d) {
+        balance_step(bal, (uint32_t)d);
+        emit(c++, pw_doubling_step_p(r, k, py_r, px3_r));
+        if ((kNafNonzero >> d) & 1u) {
+            const bool minus = (kNafMinus >> d) & 1u;
+            const G2Aff<kPt> base = {qa.x, fq2_select(minus, widen<kPt>(qy_neg), qa.y)};
+            emit(c++, pw_mixed_addition_step_p(r, base, bxpy_q, k, py_r, px_r));
+        }
+    }
+    G2Aff<kPt> q1 = mul_by_q(qa);
+    G2Aff<kPt> q2 = mul_by_q(q1);
+    q2.y = narrow<kPt>(fq2_neg(q2.y));
+    emit(c++, pw_mixed_addition_step_p(r, q1, fq2_scale(q1.x, a.py), k, py_r, px_r));
+    emit(c++, pw_mixed_addition_step_p(r, q2, fq2_scale(q2.x, a.py), k, py_r, px_r));
+#else
+    (void)scale;
+    auto emit = [&](int cc, const Ell& e) {
+        if (st) {
+            st_fq2(coeffs, nl, lt, cc * 6 + 0, e.ell_0);
+            st_fq2(coeffs, nl, lt, cc * 6 + 2, e.ell_vw);
+            st_fq2(coeffs, nl, lt, cc * 6 + 4, e.ell_vv);
+        }
+    };
 #pragma unroll 1
     for (int d = 0; d < BN_NAF_DIGITS; ++d) {
         balance_step(bal, (uint32_t)d);
@@ -85,6 +129,7 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_prepare_wide(const 
     q2.y = narrow<kPt>(fq2_neg(q2.y));
     emit(c++, pw_mixed_addition_step(r, q1, k));
     emit(c++, pw_mixed_addition_step(r, q2, k));
+#endif
 }
 #endif
 
@@ -162,12 +207,18 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kBlock) k_miller(const uint32_t* 
     fold_table_init();
     const size_t l = lane_id(), i = l / kL, nl = kL * n;
     if (i >= n) return;
-    const Fq<2> px = ld_fq<2>(paff, nl, l, 0);
-    const Fq<2> py = ld_fq<2>(paff, nl, l, 1);
-    Fq12<kF> f = miller_loop(px, py, [&](int k) {
+    auto line = [&](int k) {
         return Ell{ld_fq2<kLine>(coeffs, nl, l, k * 6 + 0), ld_fq2<kLine>(coeffs, nl, l, k * 6 + 2),
                    ld_fq2<kLine>(coeffs, nl, l, k * 6 + 4)};
-    });
+    };
+#if BN_LINES_PRESCALED
+    (void)paff;
+    Fq12<kF> f = miller_loop_scaled(line);
+#else
+    const Fq<2> px = ld_fq<2>(paff, nl, l, 0);
+    const Fq<2> py = ld_fq<2>(paff, nl, l, 1);
+    Fq12<kF> f = miller_loop(px, py, line);
+#endif
     if (flags[l]) f = widen<kF>(fq12_one());
     st_fq12(f_out, nl, l, f);
 }
@@ -236,8 +287,10 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
         mem_fence();  // load right before use: K pairs' lines are never held at once
         r.e = Ell{ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 0), ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 2),
                   ld_fq2<kLine>(coeffs, nl, lt, k * 6 + 4)};
+#if !BN_LINES_PRESCALED  // (prescaled: the line as the loop multiplies by it, no P needed)
         r.px = ld_fq<2>(paff, nl, lt, 0);
         r.py = ld_fq<2>(paff, nl, lt, 1);
+#endif
         if (!live) r.e = one_line;
         return r;
     };
@@ -268,10 +321,17 @@ __global__ void BN_PATH_ATTR __launch_bounds__(kPairBlock) k_miller_seg(const ui
             for (size_t t = 0; t < K; ++t) {
                 if (BN_SEG_LINE_BALANCE) balance_step(bal, dpos + 1u + ((uint32_t)ps << 6) + (uint32_t)t);
                 const PairLine pl = pair_line(t, idx);
+#if BN_LINES_PRESCALED
+                if (i == lo && ps == 0 && t == 0)
+                    f = line_from_one_scaled(pl.e);  // one * line (mod.rs:589 on f = one)
+                else
+                    f = apply_line_scaled(f, pl.e);
+#else
                 if (i == lo && ps == 0 && t == 0)
                     f = line_from_one(pl.e, pl.px, pl.py);  // one * line (mod.rs:589 on f = one)
                 else
                     f = apply_line(f, pl.e, pl.px, pl.py);
+#endif
             }
         }
     }

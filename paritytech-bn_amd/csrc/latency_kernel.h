@@ -108,13 +108,8 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
         LAT_STAMP(threadIdx.x == 0, 1);  // producer: to_affine done
         if (st && c == 0) g_lat_skip[j] = a.skip ? 1u : 0u;
         bool dead = false;  // a wait of this wave ran out of its cap
-        auto emit = [&](int line, const Ell& e) {
-            // slots 0, 2 scale ell_vw by Py, slots 1, 3 ell_vv by Px (one product
-            // per lane instead of two); slot 0 takes x2 from slot 1
-            const bool odd_slot = (k & 1) != 0;
-            const auto y = narrow<kLine>(fq2_scale(fq2_select(odd_slot, e.ell_vv, e.ell_vw), fq_select(odd_slot, a.px, a.py)));
-            const auto x4 = y;
-            const auto x2 = pw_from(y, 1);
+        // the ring wait (the producer stays at most kLatRing lines ahead of its consumer)
+        auto ring_wait = [&](int line) {
             uint32_t spins = 0;
             if (!dead)
                 for (; BN_ANY(valid && line - (int)cons[j] >= kLatRing) && spins < kLatSpinCap; ++spins)
@@ -124,23 +119,64 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
                 if (L == 0 && err) err_or(err, BN_ERR_INTERNAL);
             }
             asm volatile("" ::: "memory");
-            if (st) {  // the operand forms c0, c1, -c1 of each coefficient (fq12_wide.h w12_mul_line)
-                uint32_t* ln = g_lat_ring + (j * kLatRing + line % kLatRing) * kLatLineWords;
-                w_put(ln, 0 + c, e.ell_0.c);
-                w_put(ln, 3 + c, x4.c);
-                w_put(ln, 6 + c, x2.c);
-                if (c) {
-                    w_put(ln, 2, fq_neg(e.ell_0.c));
-                    w_put(ln, 5, fq_neg(x4.c));
-                    w_put(ln, 8, fq_neg(x2.c));
-                }
-            }
+        };
+        // the operand forms c0, c1, -c1 of a coefficient (fq12_wide.h w12_mul_line) at ring words 3q..3q+2
+        auto ring_put = [&](int line, int qq, const Fq2<kLine>& x) {
+            uint32_t* ln = g_lat_ring + (j * kLatRing + line % kLatRing) * kLatLineWords;
+            w_put(ln, 3 * qq + c, x.c);
+            if (c) w_put(ln, 3 * qq + 2, fq_neg(x.c));
+        };
+        auto announce = [&](int line) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the line is in LDS before it is announced
             if (st && c == 0) prod[j] = (uint32_t)line + 1;
         };
         G2Proj r = {a.qa.x, a.qa.y, widen<kPt>(fq2_one())};
         const auto qy_neg = fq2_neg(a.qa.y);
         int line = 0;
+#if BN_LINES_PRESCALED
+        // the P products from the steps' free slots (lines_wide.h PwEll): slot 0 writes
+        // ell_0, slot 2 ell_vw * Py (x4), slot 3 ell_vv * Px (x2), each from its own lanes
+        // (one select and one ring write per lane at a per-slot offset, not a write per
+        // slot under its own branch: that staged the values through scratch)
+        auto emit = [&](int ln_i, const PwEll& e) {
+            const Fq2<kLine> x = fq2_select(k == 0, e.e.ell_0, fq2_select(k == 2, e.vw_py, e.vv_px));
+            ring_wait(ln_i);
+            if (k != 1) ring_put(ln_i, k == 0 ? 0 : k - 1, x);
+            announce(ln_i);
+        };
+        const Fq2<2> py_r = pw_real(a.py);
+        const Fq2<2> px_r = pw_real(a.px);
+        const auto px3_r = pw_real(fq_add(fq_add(a.px, a.px), a.px));
+        const auto bxpy_q = fq2_scale(a.qa.x, a.py);
+#pragma unroll 1
+        for (int d = 0; d < BN_NAF_DIGITS; ++d) {
+            emit(line++, pw_doubling_step_p(r, k, py_r, px3_r));
+            if ((kNafNonzero >> d) & 1u) {
+                const bool minus = (kNafMinus >> d) & 1u;
+                const G2Aff<kPt> bq = {a.qa.x, fq2_select(minus, widen<kPt>(qy_neg), a.qa.y)};
+                emit(line++, pw_mixed_addition_step_p(r, bq, bxpy_q, k, py_r, px_r));
+            }
+        }
+        G2Aff<kPt> q1 = mul_by_q(a.qa);
+        G2Aff<kPt> q2 = mul_by_q(q1);
+        q2.y = narrow<kPt>(fq2_neg(q2.y));
+        emit(line++, pw_mixed_addition_step_p(r, q1, fq2_scale(q1.x, a.py), k, py_r, px_r));
+        emit(line++, pw_mixed_addition_step_p(r, q2, fq2_scale(q2.x, a.py), k, py_r, px_r));
+#else
+        auto emit = [&](int ln_i, const Ell& e) {
+            // slots 0, 2 scale ell_vw by Py, slots 1, 3 ell_vv by Px (one product
+            // per lane instead of two); slot 0 takes x2 from slot 1
+            const bool odd_slot = (k & 1) != 0;
+            const auto y = narrow<kLine>(fq2_scale(fq2_select(odd_slot, e.ell_vv, e.ell_vw), fq_select(odd_slot, a.px, a.py)));
+            const auto x2 = pw_from(y, 1);
+            ring_wait(ln_i);
+            if (st) {
+                ring_put(ln_i, 0, e.ell_0);
+                ring_put(ln_i, 1, y);
+                ring_put(ln_i, 2, x2);
+            }
+            announce(ln_i);
+        };
 #pragma unroll 1
         for (int d = 0; d < BN_NAF_DIGITS; ++d) {
             emit(line++, pw_doubling_step(r, k));
@@ -155,6 +191,7 @@ __global__ void __launch_bounds__(kLatThreads) BN_LAT_KERNEL_ATTR BN_LAT_KERNEL_
         q2.y = narrow<kPt>(fq2_neg(q2.y));
         emit(line++, pw_mixed_addition_step(r, q1, k));
         emit(line++, pw_mixed_addition_step(r, q2, k));
+#endif
         LAT_STAMP(threadIdx.x == 0, 2);  // producer: last line out
 #if BN_FE_DUO
         lat_multiplier((int)threadIdx.x / kWLanes, base, n, f_out, err);

@@ -186,6 +186,87 @@ __device__ __forceinline__ Ell pw_mixed_addition_step(G2Proj& s, const G2Aff<BB>
     return {narrow<kLine>(l0), narrow<kLine>(d), narrow<kLine>(fq2_neg(e))};
 }
 
+// ---------------------------------------------------------------- P-scaled lines from the free slots
+// The Miller loop multiplies by ell_0 + (ell_vw Py) w^3 + (ell_vv Px) w^4 (mod.rs:589).
+// The doubling step's middle layer above runs two distinct products on four slots and
+// the addition's first and third layers three, so the two P products fit into slots
+// that were duplicates: the scaled coefficients cost the producer no extra layer, and
+// the consumer (k_miller_seg, k_miller, the latency kernel's groups) no longer scales
+// each line (two Fq products of its ~4,700 VALU per line).  Slot 2 ends up holding
+// ell_vw * Py and slot 3 ell_vv * Px (each in its own lanes: stored from there, no
+// exchange); every slot holds ell_0 and the reference's unscaled ell_vw, ell_vv (the
+// G2Precomp export).  P products take P as the Fq2 (P, 0).
+struct PwEll {
+    Ell e;                       // the reference's coefficients
+    Fq2<kLine> vw_py, vv_px;     // ell_vw * Py on slot 2's lanes, ell_vv * Px on slot 3's
+};
+// (x, 0): this lane's coordinate of an Fq as an Fq2 (the c1 lane holds zero)
+template <int B>
+__device__ __forceinline__ Fq2<B> pw_real(const Fq<B>& x) {
+    return {fq_select(lane_odd(), widen<B>(fq_zero()), x)};
+}
+// doubling_step (curve.h) in three layers with the P products: h = (y + z)^2 - y^2 - z^2
+// = 2 y z (the same field value), so y z joins layer 1 and x^2 moves to layer 2.
+// L1: x y, y^2, z^2, y z;  L2: e = b' * 3c, j = x^2, y z * Py, z' = y^2 * h;
+// L3: x' = a (b - f), g^2, e^2, j * 3Px
+template <int PY, int PX>
+__device__ __forceinline__ PwEll pw_doubling_step_p(G2Proj& s, int k, const Fq2<PY>& py_r, const Fq2<PX>& px3_r) {
+    const auto l1 = pw_mul(k, s.x, s.y, s.y, s.y, s.z, s.z, s.y, s.z);  // x*y, y^2, z^2, y*z
+    const auto a = fq2_half(pw_from(l1, 0));
+    const auto b = pw_from(l1, 1);
+    const auto c = pw_from(l1, 2);
+    const auto yz = pw_from(l1, 3);
+    const auto h = fq2_add(yz, yz);
+    const auto d = fq2_add(fq2_add(c, c), c);
+    const auto bc = g2_coeff_b();
+    const auto l2 = pw_mul(k, bc, d, s.x, s.x, yz, py_r, b, h);  // e, j = x^2, yz * Py, z' = b * h
+    const auto e = pw_from(l2, 0);
+    const auto j = pw_from(l2, 1);
+    const auto zn = pw_from(l2, 3);
+    const auto f = fq2_add(fq2_add(e, e), e);
+    const auto g = fq2_half(fq2_add(b, f));
+    const auto i = fq2_sub(e, b);
+    const auto l3 = pw_mul(k, a, fq2_sub(b, f), g, g, e, e, j, px3_r);  // x', g^2, e^2, j * 3Px
+    const auto e_sq = pw_from(l3, 2);
+    s.x = narrow<kPt>(pw_from(l3, 0));
+    s.y = narrow<kPt>(fq2_sub(pw_from(l3, 1), fq2_add(fq2_add(e_sq, e_sq), e_sq)));
+    s.z = narrow<kPt>(zn);
+    const auto& yzpy = l2;  // slot 2: y z Py
+    PwEll r;
+    r.e = {narrow<kLine>(fq2_mul_xi(i)), narrow<kLine>(fq2_neg(h)), narrow<kLine>(fq2_add(fq2_add(j, j), j))};
+    r.vw_py = narrow<kLine>(fq2_neg(fq2_add(yzpy, yzpy)));  // -h Py
+    r.vv_px = narrow<kLine>(l3);                             // slot 3: 3 j Px
+    return r;
+}
+// mixed_addition_step (curve.h) in four layers with the P products:
+// L1: z bx, z by, x Py, z (bx Py)  (d Py = x Py - z bx Py);  L2: d^2, e^2, e bx, d by;
+// L3: d f, x f, z g, e Px;  L4: as pw_mixed_addition_step.  bxpy = base.x * Py (per base)
+template <int BB, int XB, int PY, int PX>
+__device__ __forceinline__ PwEll pw_mixed_addition_step_p(G2Proj& s, const G2Aff<BB>& base, const Fq2<XB>& bxpy,
+                                                          int k, const Fq2<PY>& py_r, const Fq2<PX>& px_r) {
+    const auto l1 = pw_mul(k, s.z, base.x, s.z, base.y, s.x, py_r, s.z, bxpy);  // z*bx, z*by, x*Py, z*bxPy
+    const auto d = fq2_sub(s.x, pw_from(l1, 0));
+    const auto e = fq2_sub(s.y, pw_from(l1, 1));
+    const auto zbxpy = pw_from(l1, 3);
+    const auto l2 = pw_mul(k, d, d, e, e, e, base.x, d, base.y);  // f = d^2, g = e^2, e*bx, d*by
+    const auto f = pw_from(l2, 0);
+    const auto g = pw_from(l2, 1);
+    const auto l0 = fq2_mul_xi(fq2_sub(pw_from(l2, 2), pw_from(l2, 3)));
+    const auto l3 = pw_mul(k, d, f, s.x, f, s.z, g, e, px_r);  // h = d*f, i = x*f, z*g, e*Px
+    const auto h = pw_from(l3, 0);
+    const auto i = pw_from(l3, 1);
+    const auto jj = fq2_sub(fq2_add(pw_from(l3, 2), h), fq2_add(i, i));
+    const auto l4 = pw_mul(k, d, jj, e, fq2_sub(i, jj), h, s.y, s.z, h);  // nx, e*(i - j), h*y, nz
+    s.x = narrow<kPt>(pw_from(l4, 0));
+    s.y = narrow<kPt>(fq2_sub(pw_from(l4, 1), pw_from(l4, 2)));
+    s.z = narrow<kPt>(pw_from(l4, 3));
+    PwEll r;
+    r.e = {narrow<kLine>(l0), narrow<kLine>(d), narrow<kLine>(fq2_neg(e))};
+    r.vw_py = narrow<kLine>(fq2_sub(l1, zbxpy));  // slot 2: x Py - z bx Py = d Py
+    r.vv_px = narrow<kLine>(fq2_neg(l3));         // slot 3: -e Px
+    return r;
+}
+
 
 #endif  // BN_SPLIT
 

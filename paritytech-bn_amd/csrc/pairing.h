@@ -144,6 +144,21 @@ BN_INLINE Fq12<kF> apply_line(const Fq12<B>& f, const Ell& c, const Fq<PB>& px, 
 #endif
 }
 
+// the same with the line already scaled by P (e.ell_vw = ell_vw * Py, e.ell_vv = ell_vv * Px:
+// what the producers store with BN_LINES_PRESCALED, lines_wide.h PwEll)
+template <int B>
+BN_INLINE Fq12<kF> apply_line_scaled(const Fq12<B>& f, const Ell& e) {
+#if BN_SPLIT
+    return widen<kF>(fq12_mul_by_024_lazy(narrow12<2>(f), e.ell_0, e.ell_vw, e.ell_vv));
+#else
+    return narrow12<kF>(fq12_mul_by_024(f, e.ell_0, e.ell_vw, e.ell_vv));
+#endif
+}
+BN_INLINE Fq12<kF> line_from_one_scaled(const Ell& e) {
+    const Fq2<kF> z = widen<kF>(fq2_zero());
+    return {{narrow<kF>(e.ell_0), z, narrow<kF>(e.ell_vv)}, {z, narrow<kF>(e.ell_vw), z}};
+}
+
 // The first step of a loop (or segment) that starts from f = one: one^2 * line
 // is the line itself, x0 + x4 w^3 + x2 w^4 (w^3 = c1.c1, w^4 = c0.c2; the
 // operands of apply_line), so the squaring and the sparse product are skipped
@@ -174,6 +189,21 @@ BN_INLINE Fq12<kF> miller_loop(const Fq<PB>& px, const Fq<PB>& py, Line&& line) 
     }
     f = apply_line(f, line(idx++), px, py);
     f = apply_line(f, line(idx), px, py);
+    return f;
+}
+// the same over lines already scaled by P (apply_line_scaled)
+template <typename Line>
+BN_INLINE Fq12<kF> miller_loop_scaled(Line&& line) {
+    Fq12<kF> f = widen<kF>(fq12_one());
+    int idx = 0;
+#pragma unroll 1
+    for (int i = 0; i < BN_NAF_DIGITS; ++i) {
+        const Ell e = line(idx++);
+        f = i == 0 ? line_from_one_scaled(e) : apply_line_scaled(narrow12<kF>(fq12_sqr(f)), e);
+        if ((kNafNonzero >> i) & 1u) f = apply_line_scaled(f, line(idx++));
+    }
+    f = apply_line_scaled(f, line(idx++));
+    f = apply_line_scaled(f, line(idx));
     return f;
 }
 
