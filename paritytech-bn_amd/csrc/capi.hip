@@ -884,6 +884,13 @@ int bn_ctx_create(int device, bn_ctx** out) {
             c->lat_w1_max = (size_t)cus * kLatPairs;
     }
     c->prepare_wide_max = kPrepareWideMaxDefault;
+    // $BN254MI_FE_DS_MAX: pairing_many batches up to this size take k_fe_ds for the
+    // final exponentiations (0: the latency kernel's own 16-lane FE; A/B)
+    c->fe_ds_max = kFeDsMax;
+    if (const char* e = getenv("BN254MI_FE_DS_MAX")) {
+        const size_t v = (size_t)strtoull(e, nullptr, 10);
+        c->fe_ds_max = v < (size_t)kFeDsMax ? v : (size_t)kFeDsMax;
+    }
     if (const char* e = getenv("BN254MI_PREPARE_WIDE_MAX")) c->prepare_wide_max = (size_t)strtoull(e, nullptr, 10);
     Prog P;
     c->fe_out = (int)build_final_exp(P);
@@ -906,6 +913,8 @@ int bn_ctx_create(int device, bn_ctx** out) {
         hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming) != hipSuccess ||
         hipMalloc(&c->d_err, sizeof(int)) != hipSuccess || hipMemset(c->d_err, 0, sizeof(int)) != hipSuccess ||
         hipMalloc(&c->tail_ws, kTailWsWords * 4) != hipSuccess || hipMemset(c->tail_ws, 0, kTailWsWords * 4) != hipSuccess ||
+        hipMalloc(&c->fe_ds_ws, (size_t)kFeDsMax * kFeDsWords * 4) != hipSuccess ||
+        hipMemset(c->fe_ds_ws, 0, (size_t)kFeDsMax * kFeDsWords * 4) != hipSuccess ||
         hipMalloc(&c->d_prog, P.s.size() * 4) != hipSuccess ||
         hipMemcpy(c->d_prog, P.s.data(), P.s.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         ctx_teardown(c);  // releases whatever was created (null handles are skipped)
@@ -939,7 +948,7 @@ static void ctx_teardown(bn_ctx* c) {
     for (hipStream_t s : {c->h2d, c->d2h})
         if (s) (void)hipStreamDestroy(s);
     for (void* p : {(void*)c->coeffs, (void*)c->paff, (void*)c->slots, (void*)c->flags, (void*)c->d_err,
-                    (void*)c->d_prog, c->stage, (void*)c->tail_ws})
+                    (void*)c->d_prog, c->stage, (void*)c->tail_ws, (void*)c->fe_ds_ws})
         if (p) (void)hipFree(p);
     for (auto& ev : c->ev_marks)
         for (auto e : ev) c->ev_pool.push_back(e);
@@ -992,6 +1001,24 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             if (c->timing && ev[k]) (void)hipEventRecord(ev[k], s);
         };
         mark(0);
+        if (m <= c->fe_wide_max && m <= c->latency_max && m <= c->fe_ds_max) {
+            // the Miller values in one launch (k_pairing_latency), then each pairing's final
+            // exponentiation on three digit-sliced blocks (kernels_tail.hip k_fe_ds)
+            launch_latency(c, d_p + off, d_q + off, m, nullptr, slot_region(c, kRegionSeg), 0, s);
+            HIPCHK(c, hipGetLastError());
+            c->tail_epoch = c->tail_epoch + 1 < (1u << 29) ? c->tail_epoch + 1 : 1u;
+            // three blocks per pair while they fit one round (one 84 KB block per CU), else one
+            const int per = 3 * m * kLatPairs <= c->lat_w1_max ? 3 : 1;  // (lat_w1_max = CUs x kLatPairs)
+            k_fe_ds<<<(unsigned)(per * m), kTailBlock, 0, s>>>(slot_region(c, kRegionSeg), m, d_out + off, c->d_err,
+                                                               c->fe_ds_ws, c->tail_epoch, per);
+            mark(1);
+            mark(2);
+            mark(3);
+            mark(4);
+            HIPCHK(c, hipGetLastError());
+            if (c->timing) c->ev_marks.push_back(ev);
+            continue;
+        }
         if (m <= c->fe_wide_max && m <= c->latency_max) {
             // the whole pairing in one launch: line producer + wide Miller loop and FE
             // (kernels_wide.hip k_pairing_latency)

@@ -53,6 +53,10 @@ struct bn_ctx {
     // launch's epoch, so no clearing between products
     uint32_t* tail_ws = nullptr;
     uint32_t tail_epoch = 0;
+    // pairing_many of at most fe_ds_max pairs: k_pairing_latency's Miller values, then
+    // k_fe_ds (three digit-sliced blocks per pair); its words (kFeDsMax pairs, zeroed)
+    uint32_t* fe_ds_ws = nullptr;
+    size_t fe_ds_max = 0;
     // staging for host-buffer calls (device)
     size_t stage_bytes = 0;
     void* stage = nullptr;

@@ -609,6 +609,15 @@ constexpr int kTailWsWords = kTailChanWords + 2 * kMaxSeg * 256;
 __global__ void __launch_bounds__(kTailBlock) k_seg_tail(const uint32_t* __restrict__ g, SegPlan plan,
                                                          bn_gt* __restrict__ out, int* __restrict__ err,
                                                          uint32_t* __restrict__ ws, uint32_t epoch);
+// pairing_many's final exponentiations of n <= kFeDsMax Miller values (split layout,
+// stride n) on `per` blocks per pair (3: squarer + two multiplier candidates, 1: the
+// squarer alone; digit-sliced) into out[0..n); ws = bn_ctx.fe_ds_ws (kFeDsWords per pair,
+// zeroed at creation)
+constexpr int kFeDsMax = 256;
+constexpr int kFeDsWords = kTailChanWords;  // role word (kernels_tail.hip kRoleWord) + channel
+__global__ void __launch_bounds__(kTailBlock) k_fe_ds(const uint32_t* __restrict__ f, size_t n,
+                                                      bn_gt* __restrict__ out, int* __restrict__ err,
+                                                      uint32_t* __restrict__ ws, uint32_t epoch, int per);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
 // (a producer wave for the lines, consumer groups for the wide Miller loop + FE)
 constexpr int kLatPairs = 8;

@@ -306,6 +306,47 @@ __device__ uint32_t tail_await_decision(uint32_t* rw, uint32_t epoch, int* err) 
     if (err) err_or(err, BN_ERR_INTERNAL);
     return 0;
 }
+// a multiplier candidate of the last chunk: claims M_0 or M_1 on the role word rw, waits
+// for the squarer's decision, runs its share if the squarer takes both multipliers
+__device__ __forceinline__ void tail_multiplier(uint32_t* rw, DsChan& ch, uint32_t epoch, int* err) {
+#if BN_TAIL_LATE_M
+    for (int t = 0; t < 40000; ++t) __builtin_amdgcn_s_sleep(1);
+#endif
+    __syncthreads();
+    if (threadIdx.x == 0) g_tail_role = tail_claim_m(rw, epoch);
+    __syncthreads();
+    const uint32_t role = g_tail_role;
+    if (role == 0) return;
+    __syncthreads();
+    if (threadIdx.x == 0) g_tail_role = tail_await_decision(rw, epoch, err);
+    __syncthreads();
+    if (g_tail_role != (kTailM0 | kTailM1)) return;  // the squarer went on alone
+    if (BN_TAIL_STAMPS) TAIL_STAMP(role == 1 ? 25 : 27);
+    ds_fe_last_m2(ch, (int)role - 1);
+    if (BN_TAIL_STAMPS) TAIL_STAMP(role == 1 ? 26 : 28);
+}
+// the squarer: decides (both multipliers if both have claimed, else alone), runs the
+// last chunk of d and writes the Gt image to *out (zero: BN_ERR_FE_ZERO, the zero image)
+__device__ __forceinline__ void tail_squarer(uint32_t d, uint32_t* rw, DsChan& ch, uint32_t epoch, int* err,
+                                             bn_gt* out, const WL& w) {
+    __syncthreads();
+    if (threadIdx.x == 0) g_tail_role = tail_decide(rw, epoch);
+    __syncthreads();
+    if (g_tail_role == (kTailM0 | kTailM1))
+        d = ds_fe_last_s2(d, ch);
+    else
+        d = ds_fe_last(d);
+    if (BN_TAIL_STAMPS) TAIL_STAMP(8);
+    const Fq<2> r = ds_to_w12(d);  // threads 0..11 get the value
+    const bool z = w12_is_zero(r);
+    if (threadIdx.x == 0) g_tail_zero = z ? 1u : 0u;
+    __syncthreads();
+    const bool zero = g_tail_zero != 0;
+    if (zero && err && threadIdx.x == 0) err_or(err, BN_ERR_FE_ZERO);
+    uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!zero && threadIdx.x < 12) fq_store_ref(r, words);
+    if (threadIdx.x < 12) st_words(&out->c[w_gt_index(w)], words);
+}
 __global__ void __launch_bounds__(kTailThreads) k_seg_tail(const uint32_t* __restrict__ g, SegPlan plan,
                                                            bn_gt* __restrict__ out, int* __restrict__ err,
                                                            uint32_t* __restrict__ ws, uint32_t epoch) {
@@ -349,42 +390,43 @@ __global__ void __launch_bounds__(kTailThreads) k_seg_tail(const uint32_t* __res
         ds_init();
     }
     if (!carrier) {  // one of the last chunk's multipliers, if a role is still free
-#if BN_TAIL_LATE_M
-        for (int t = 0; t < 40000; ++t) __builtin_amdgcn_s_sleep(1);
-#endif
-        __syncthreads();
-        if (threadIdx.x == 0) g_tail_role = tail_claim_m(ws + kRoleWord, epoch);
-        __syncthreads();
-        const uint32_t role = g_tail_role;
-        if (role == 0) return;
-        __syncthreads();
-        if (threadIdx.x == 0) g_tail_role = tail_await_decision(ws + kRoleWord, epoch, err);
-        __syncthreads();
-        if (g_tail_role != (kTailM0 | kTailM1)) return;  // the squarer went on alone
-        if (BN_TAIL_STAMPS) TAIL_STAMP(role == 1 ? 25 : 27);
-        ds_fe_last_m2(ch, (int)role - 1);
-        if (BN_TAIL_STAMPS) TAIL_STAMP(role == 1 ? 26 : 28);
+        tail_multiplier(ws + kRoleWord, ch, epoch, err);
         return;
     }
     // the carrier of P_0: the squarer
     if (BN_TAIL_STAMPS) TAIL_STAMP(1);
-    __syncthreads();
-    if (threadIdx.x == 0) g_tail_role = tail_decide(ws + kRoleWord, epoch);
-    __syncthreads();
-    if (g_tail_role == (kTailM0 | kTailM1))
-        d = ds_fe_last_s2(d, ch);
-    else
-        d = ds_fe_last(d);
-    if (BN_TAIL_STAMPS) TAIL_STAMP(8);
-    const Fq<2> r = ds_to_w12(d);  // threads 0..11 get the value
-    const bool z = w12_is_zero(r);
-    if (threadIdx.x == 0) g_tail_zero = z ? 1u : 0u;
-    __syncthreads();
-    const bool zero = g_tail_zero != 0;
-    if (zero && err && threadIdx.x == 0) err_or(err, BN_ERR_FE_ZERO);
-    uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (!zero && threadIdx.x < 12) fq_store_ref(r, words);
-    if (threadIdx.x < 12) st_words(&out[0].c[w_gt_index(w)], words);
+    tail_squarer(d, ws + kRoleWord, ch, epoch, err, &out[0], w);
+}
+
+// pairing_many's final exponentiations for batches of at most kFeDsMax pairs (after
+// k_pairing_latency wrote the Miller values, f_out): with per = 3, pair i takes blocks
+// 3i (the squarer, which runs the first chunk first, w12_fe_first_par) and 3i + 1,
+// 3i + 2 (multiplier candidates); with per = 1 (more pairs than a third of the CUs) one
+// block per pair, the squarer alone.  Each pair has its own role word and channel
+// (kFeDsWords of ws, epoch-stamped as k_seg_tail's).  The digit-sliced last chunk with
+// two multipliers against the latency kernel's 16-lane two-group one: ~0.24 ms shorter
+// per pairing (profiles/r6q_latency_fe_ds.txt).
+// f == 0 (the reference's final_exponentiation returns None): BN_ERR_FE_ZERO and the
+// zero image, as the latency kernel.
+__global__ void __launch_bounds__(kTailThreads) k_fe_ds(const uint32_t* __restrict__ f, size_t n,
+                                                        bn_gt* __restrict__ out, int* __restrict__ err,
+                                                        uint32_t* __restrict__ ws, uint32_t epoch, int per) {
+    fold_table_init();
+    const WL w = wl();
+    const size_t i = blockIdx.x / (unsigned)per;
+    if (i >= n) return;  // (block-uniform)
+    uint32_t* pw = ws + i * (size_t)kFeDsWords;
+    DsChan ch = {(uint64_t*)(pw + kDsChanOff), err, 0, 0, false, epoch};
+    if (blockIdx.x % (unsigned)per != 0) {
+        ds_init();
+        tail_multiplier(pw + kRoleWord, ch, epoch, err);
+        return;
+    }
+    Fq<2> x = widen<2>(fq_zero());
+    if (threadIdx.x < (unsigned)kWLanes) x = w_ld_split(f, n, i, w);  // group 0
+    x = w12_fe_first_par(x);
+    ds_init();
+    tail_squarer(ds_from_w12(x), pw + kRoleWord, ch, epoch, err, &out[i], w);
 }
 #endif
 
