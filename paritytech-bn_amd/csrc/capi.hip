@@ -404,10 +404,22 @@ int product_wide(bn_ctx* c, const uint32_t* in, size_t in_stride, SetSpan span, 
     }
 }
 
+// k_fe_ds over n <= c->fe_ds_max split-layout values of f (stride n): three blocks per
+// value while they fit one round (one 84 KB block per CU), else one
+static void launch_fe_ds(bn_ctx* c, const uint32_t* f, size_t n, bn_gt* out, uint8_t* ok, hipStream_t s) {
+    c->tail_epoch = c->tail_epoch + 1 < (1u << 29) ? c->tail_epoch + 1 : 1u;
+    const int per = 3 * n * kLatPairs <= c->lat_w1_max ? 3 : 1;  // (lat_w1_max = CUs x kLatPairs)
+    k_fe_ds<<<(unsigned)(per * n), kTailBlock, 0, s>>>(f, n, out, ok, c->d_err, c->fe_ds_ws, c->tail_epoch, per);
+}
 // final exponentiation of the n split-layout values of `f` (stride n) -> out
 // (device Gt images): the wide layout for small batches, else the step machine
 // (whose program reads and writes the slots from slot 0: f must be slot 0)
 int run_fe(bn_ctx* c, const uint32_t* f, size_t n, const uint8_t* flags, bn_gt* out, uint8_t* ok, hipStream_t s) {
+    if (n <= c->fe_ds_max && n <= c->fe_wide_max) {  // digit-sliced blocks per value (kernels_tail.hip k_fe_ds)
+        launch_fe_ds(c, f, n, out, ok, s);
+        HIPCHK(c, hipGetLastError());
+        return BN_OK;
+    }
     if (n <= c->fe_wide_max) {
         k_fe_wide<<<wide_blocks(n), kBlock, 0, s>>>(f, n, n, out, ok, c->d_err, wide_duo(n) ? 1 : 0);
         HIPCHK(c, hipGetLastError());
@@ -1006,11 +1018,7 @@ static int pairing_many_dev_impl(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, 
             // exponentiation on three digit-sliced blocks (kernels_tail.hip k_fe_ds)
             launch_latency(c, d_p + off, d_q + off, m, nullptr, slot_region(c, kRegionSeg), 0, s);
             HIPCHK(c, hipGetLastError());
-            c->tail_epoch = c->tail_epoch + 1 < (1u << 29) ? c->tail_epoch + 1 : 1u;
-            // three blocks per pair while they fit one round (one 84 KB block per CU), else one
-            const int per = 3 * m * kLatPairs <= c->lat_w1_max ? 3 : 1;  // (lat_w1_max = CUs x kLatPairs)
-            k_fe_ds<<<(unsigned)(per * m), kTailBlock, 0, s>>>(slot_region(c, kRegionSeg), m, d_out + off, c->d_err,
-                                                               c->fe_ds_ws, c->tail_epoch, per);
+            launch_fe_ds(c, slot_region(c, kRegionSeg), m, d_out + off, nullptr, s);
             mark(1);
             mark(2);
             mark(3);

@@ -616,8 +616,9 @@ __global__ void __launch_bounds__(kTailBlock) k_seg_tail(const uint32_t* __restr
 constexpr int kFeDsMax = 256;
 constexpr int kFeDsWords = kTailChanWords;  // role word (kernels_tail.hip kRoleWord) + channel
 __global__ void __launch_bounds__(kTailBlock) k_fe_ds(const uint32_t* __restrict__ f, size_t n,
-                                                      bn_gt* __restrict__ out, int* __restrict__ err,
-                                                      uint32_t* __restrict__ ws, uint32_t epoch, int per);
+                                                      bn_gt* __restrict__ out, uint8_t* __restrict__ ok,
+                                                      int* __restrict__ err, uint32_t* __restrict__ ws,
+                                                      uint32_t epoch, int per);
 // kernels_wide.hip: the whole pairing of kLatPairs pairs per block in one launch
 // (a producer wave for the lines, consumer groups for the wide Miller loop + FE)
 constexpr int kLatPairs = 8;

@@ -326,9 +326,10 @@ __device__ __forceinline__ void tail_multiplier(uint32_t* rw, DsChan& ch, uint32
     if (BN_TAIL_STAMPS) TAIL_STAMP(role == 1 ? 26 : 28);
 }
 // the squarer: decides (both multipliers if both have claimed, else alone), runs the
-// last chunk of d and writes the Gt image to *out (zero: BN_ERR_FE_ZERO, the zero image)
+// last chunk of d and writes the Gt image to *out (zero: BN_ERR_FE_ZERO, the zero image;
+// *ok = 0 for zero, 1 otherwise, when ok is given)
 __device__ __forceinline__ void tail_squarer(uint32_t d, uint32_t* rw, DsChan& ch, uint32_t epoch, int* err,
-                                             bn_gt* out, const WL& w) {
+                                             bn_gt* out, const WL& w, uint8_t* ok = nullptr) {
     __syncthreads();
     if (threadIdx.x == 0) g_tail_role = tail_decide(rw, epoch);
     __syncthreads();
@@ -343,6 +344,7 @@ __device__ __forceinline__ void tail_squarer(uint32_t d, uint32_t* rw, DsChan& c
     __syncthreads();
     const bool zero = g_tail_zero != 0;
     if (zero && err && threadIdx.x == 0) err_or(err, BN_ERR_FE_ZERO);
+    if (ok && threadIdx.x == 0) *ok = zero ? 0 : 1;
     uint32_t words[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (!zero && threadIdx.x < 12) fq_store_ref(r, words);
     if (threadIdx.x < 12) st_words(&out->c[w_gt_index(w)], words);
@@ -406,11 +408,12 @@ __global__ void __launch_bounds__(kTailThreads) k_seg_tail(const uint32_t* __res
 // (kFeDsWords of ws, epoch-stamped as k_seg_tail's).  The digit-sliced last chunk with
 // two multipliers against the latency kernel's 16-lane two-group one: ~0.24 ms shorter
 // per pairing (profiles/r6q_latency_fe_ds.txt).
-// f == 0 (the reference's final_exponentiation returns None): BN_ERR_FE_ZERO and the
-// zero image, as the latency kernel.
+// f == 0 (the reference's final_exponentiation returns None): BN_ERR_FE_ZERO, the
+// zero image and ok[i] = 0 (when ok is given), as the latency kernel and k_fe_wide.
 __global__ void __launch_bounds__(kTailThreads) k_fe_ds(const uint32_t* __restrict__ f, size_t n,
-                                                        bn_gt* __restrict__ out, int* __restrict__ err,
-                                                        uint32_t* __restrict__ ws, uint32_t epoch, int per) {
+                                                        bn_gt* __restrict__ out, uint8_t* __restrict__ ok,
+                                                        int* __restrict__ err, uint32_t* __restrict__ ws,
+                                                        uint32_t epoch, int per) {
     fold_table_init();
     const WL w = wl();
     const size_t i = blockIdx.x / (unsigned)per;
@@ -426,7 +429,7 @@ __global__ void __launch_bounds__(kTailThreads) k_fe_ds(const uint32_t* __restri
     if (threadIdx.x < (unsigned)kWLanes) x = w_ld_split(f, n, i, w);  // group 0
     x = w12_fe_first_par(x);
     ds_init();
-    tail_squarer(ds_from_w12(x), pw + kRoleWord, ch, epoch, err, &out[i], w);
+    tail_squarer(ds_from_w12(x), pw + kRoleWord, ch, epoch, err, &out[i], w, ok ? ok + i : nullptr);
 }
 #endif
 
