@@ -652,7 +652,10 @@ uint32_t* parts_region(bn_ctx* c, size_t nchunks) {
 #ifndef BN_TAIL_M
 #define BN_TAIL_M 1
 #endif
-static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out, hipStream_t s) {
+// (g: the segment values, element s at stride S; default the result region)
+static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out, hipStream_t s,
+                         uint32_t* g = nullptr) {
+    if (!g) g = slot_region(c, kRegionResult);
     const char* env = getenv("BN254MI_HORNER_TREE");
     const int tree = env ? atoi(env) : 2;  // 2: k_horner_tree2 (default), 1: k_horner_tree, 0: k_horner_wide
     static const bool fused = [] {  // $BN254MI_TAIL_FUSED=0: k_seg_fe1 + k_horner_tree2 (A/B)
@@ -663,7 +666,7 @@ static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out
         plan.S <= kMaxSeg) {
         // pairing_batch: the whole tail in one launch (kernels_tail.hip k_seg_tail)
         c->tail_epoch = c->tail_epoch + 1 < (1u << 29) ? c->tail_epoch + 1 : 1u;  // (epoch * 8 fits the role word)
-        k_seg_tail<<<plan.S > 3 ? plan.S : 3, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, d_out, c->d_err,
+        k_seg_tail<<<plan.S > 3 ? plan.S : 3, kTailBlock, 0, s>>>(g, plan, d_out, c->d_err,
                                                                   c->tail_ws, c->tail_epoch);
     } else if (tree == 2 && BN_FE_DUO && plan.S <= kMaxSeg) {
         // pairing_batch: the segments' first chunks and squarings one block each
@@ -673,7 +676,7 @@ static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out
         const uint32_t* zf = nullptr;
         if (BN_TAIL_DS && BN_SEG_FE1 && do_fe && plan.S >= 1 && (size_t)kSlotWords * c->cap >= (size_t)kTailChanWords) {
             uint32_t* z = slot_region(c, kRegionA);
-            k_seg_fe1<<<plan.S, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, z);
+            k_seg_fe1<<<plan.S, kTailBlock, 0, s>>>(g, plan, z);
             HIPCHK(c, hipGetLastError());
             zf = z;
         }
@@ -683,14 +686,14 @@ static int recombine_one(bn_ctx* c, const SegPlan& plan, int do_fe, bn_gt* d_out
         // word k_seg_fe1 clears (kernels_tail.hip tail_claim): a multiplier that has not
         // started when the squarer gets there is not waited for -- the squarer runs
         // the chunk alone (the same value) and the late block returns.
-        k_horner_tree2<<<zf && BN_TAIL_M ? 2 : 1, kTailBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err,
+        k_horner_tree2<<<zf && BN_TAIL_M ? 2 : 1, kTailBlock, 0, s>>>(g, plan, do_fe, d_out, c->d_err,
                                                           zf);
     }
     else if (tree != 0)
-        k_horner_tree<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), plan, do_fe, d_out, c->d_err,
+        k_horner_tree<<<1, kBlock, 0, s>>>(g, plan, do_fe, d_out, c->d_err,
                                            wide_duo(1) ? 1 : 0);
     else
-        k_horner_wide<<<1, kBlock, 0, s>>>(slot_region(c, kRegionResult), 1, plan, do_fe, d_out, c->d_err,
+        k_horner_wide<<<1, kBlock, 0, s>>>(g, 1, plan, do_fe, d_out, c->d_err,
                                            wide_duo(1) ? 1 : 0);
     HIPCHK(c, hipGetLastError());
     return BN_OK;
@@ -726,6 +729,8 @@ int latency_product(bn_ctx* c, const bn_g1* d_p, const bn_g2* d_q, size_t n, int
     RET_IF(reserve(c, n));
     launch_latency(c, d_p, d_q, n, nullptr, slot_region(c, kRegionSeg), mode, s);
     HIPCHK(c, hipGetLastError());
+    // one pair: its Miller value is the product, read in place (no reduction launch, ~15 us)
+    if (n == 1) return recombine_one(c, cut_plan(1, 1), do_fe, d_out, s, slot_region(c, kRegionSeg));
     RET_IF(product_wide(c, slot_region(c, kRegionSeg), n, uniform_span(1, n), 1, slot_region(c, kRegionResult), 1, 0,
                         1, s));
     return recombine_one(c, cut_plan(1, 1), do_fe, d_out, s);  // one segment: the FE of the product when do_fe
