@@ -156,3 +156,69 @@ def test_allgather_dev_distinct_devices(data):
     ctx.dev_status()
     for k in range(nd):
         assert np.array_equal(outs[k].cpu().numpy().view(np.uint64), data["gt"][:n]), "device %d" % k
+
+
+def _ranks_worker(rank, world, port, n, qout):
+    """One rank of the torch.distributed form with the ENGINE as its compute (no
+    injected hook): every rank's context on device 0, the collective over gloo
+    (RCCL refuses two ranks on one device)."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "paritytech-bn_amd")]
+    try:
+        import torch.distributed as dist
+
+        from oracle import oracle as O
+        from substrate_bn import parallel
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+        p, q, _, _ = O.random_pairs(n, seed=912, nthreads=2)
+        p[3] = 0
+        p[3, 4:8] = O.canon_to_mont_array([1])  # a zero point: one for pairing, skipped by pairing_batch
+        many = parallel.pairing_many_distributed(p, q)
+        prod = parallel.pairing_batch_distributed(p, q)
+        dist.destroy_process_group()
+        qout.put((rank, many, prod))
+    except Exception as e:  # report instead of hanging the parent
+        qout.put((rank, None, repr(e)))
+        raise
+
+
+@pytest.mark.parametrize("world,n", [(4, 4099), (8, 5)])
+def test_torch_distributed_ranks_on_one_gpu(world, n):
+    """config 4's control flow with the engine as each rank's compute: `world` rank
+    processes (one context each, all on the one MI355X of this box), contiguous shards,
+    the Gt rows gathered in rank order and pairing_batch's partials multiplied in rank
+    order.  n = 5 at world 8 leaves three ranks with an empty shard.  Every rank's
+    results equal the oracle bit for bit."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    qout = ctx.Queue()
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=_ranks_worker, args=(r, world, port, n, qout)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, many, prod = qout.get(timeout=150)
+            assert many is not None, prod
+            res[rank] = (many, prod)
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+            if pr.exitcode is None:
+                pr.kill()
+    assert all(pr.exitcode == 0 for pr in procs)
+    p, q, _, _ = O.random_pairs(n, seed=912, nthreads=NT)
+    p[3] = 0
+    p[3, 4:8] = O.canon_to_mont_array([1])
+    want_many = O.pairing_many(p, q, NT)
+    want_prod = O.pairing_batch(p, q)
+    for r in range(world):
+        assert np.array_equal(res[r][0], want_many), "rank %d" % r
+        assert np.array_equal(res[r][1], want_prod), "rank %d" % r
