@@ -1011,14 +1011,21 @@ def main():
     import torch
     import torch.distributed as dist
 
-    eng = (DryEngine if args.dry_run_cpu else GpuEngine)(local_rank)
+    # BN254MI_BENCH_SHARED_GPU=1: a rehearsal of the N > 1 launch on a one-GPU box -- every
+    # rank computes on device 0 and the collectives go over gloo (RCCL refuses two ranks
+    # on one device); the line is marked and is no scaling figure
+    shared = world > 1 and not args.dry_run_cpu and os.environ.get("BN254MI_BENCH_SHARED_GPU") == "1"
+    eng = (DryEngine if args.dry_run_cpu else GpuEngine)(0 if shared else local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if eng.dry:
+        if eng.dry or shared:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     res = run_pairing(args, eng, rank, world, dist)
+    if shared:
+        res["rehearsal"] = ("BN254MI_BENCH_SHARED_GPU: %d ranks on ONE MI355X, gloo collectives -- the N > 1 "
+                            "control flow with real pairings, not a scaling figure" % world)
     if rank == 0:
         emit(res)
     if world > 1:

@@ -222,3 +222,32 @@ def test_torch_distributed_ranks_on_one_gpu(world, n):
     for r in range(world):
         assert np.array_equal(res[r][0], want_many), "rank %d" % r
         assert np.array_equal(res[r][1], want_prod), "rank %d" % r
+
+
+def test_bench_driver_launch_two_ranks_on_one_gpu():
+    """The driver's own N > 1 command (torch.distributed.run --nproc-per-node 2 ...
+    bench.py --gpus 2) with BN254MI_BENCH_SHARED_GPU=1: both ranks on device 0 over
+    gloo.  Config 4's sharding, the in-step all-gather, the max-over-ranks timing and
+    both checks (cross-rank recompute, oracle sample of the gathered rows) run with
+    real pairings."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, BN254MI_BENCH_SHARED_GPU="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--total", "16384", "--chunk", "4096", "--cpu-sample", "256", "--no-e2e"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and "rehearsal" in line
+    assert line["collective"]["world_from_allreduce"] == 2
+    assert line["cross_rank_check"]["mismatches"] == 0 and line["cross_rank_check"]["ranks_ok"] == 2
+    assert line["sample_check"]["parity_sample_bit_exact"] is True
