@@ -207,6 +207,18 @@ def test_large_batch_parity_and_bilinearity(ctx):
     assert np.array_equal(e1[idx], O.pairing_many(sP[idx], Q[idx], NT))
 
 
+def test_config2_full_size_every_row(ctx_tp):
+    """BASELINE config 2 at its full size on the kernel bench.py measures
+    (k_pairing_full): 2^16 random pairs with random Jacobian z (not one), every
+    Gt image bit-exact against the oracle (~7 s of 16 host threads)."""
+    n = 1 << 16
+    _, S = O.random_scalars(n, seed=2020, lo=1)
+    P = ctx_tp.g1_mul_many(np.tile(O.g1_one(), (n, 1)), S)
+    Q = ctx_tp.g2_mul_many(np.tile(O.g2_one(), (n, 1)), np.roll(S, 5, axis=0))
+    got = ctx_tp.pairing_many(P, Q)
+    assert np.array_equal(got, O.pairing_many(P, Q, NT))
+
+
 def test_prepared_g2_on_gpu(ctx, kats, pairs):
     """All 87 line coefficients computed on the GPU (bn_g2_precompute_many):
     the reference's test_prepared_g2 vector (src/groups/mod.rs:780-892) and 64
